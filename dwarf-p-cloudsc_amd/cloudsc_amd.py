@@ -1,0 +1,432 @@
+"""Host-side mirror of the CLOUDSC dwarf plumbing, over the libcloudsc_amd.so C ABI.
+
+This is the Python face of the same boundary the C host driver
+(``dwarf-p-cloudsc_amd/csrc/dwarf_cloudsc_amd.c``) uses.  It mirrors the
+reference driver's plumbing:
+
+* dataset loading -- the Serialbox raw arrays + global scalars the reference
+  reads (``src/cloudsc_c/cloudsc/load_state.c:279-690``; the ``data/*.dat`` files
+  are C-order ``[lev][klon]`` / ``[nclv][lev][klon]`` arrays, exactly the HDF5
+  dataset layout of ``config-files/reference.h5``);
+* NPROMA-block expansion with the global ``g % klon`` column map
+  (``load_state.c:69-184``, ``src/common/module/expand_mod.F90:173-200``);
+* field-wise validation with the Fortran ERROR_PRINT semantics
+  (``src/common/module/validate_mod.F90:118-296``) -- ``fabs``, not the C
+  validator's integer ``abs`` (``cloudsc_validate.c:74,109,147``);
+* the GPU state API (device-side expand / run / validate) of ``cloudsc_amd.h``.
+
+The GPU path has no fallback: if ``libcloudsc_amd.so`` is missing or no HIP
+device is visible, :func:`gpu_lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libcloudsc_amd.so")
+GOLDEN_DIR = os.path.join(REPO, "tests", "golden", "cloudsc100")
+
+NCLV = 5
+FP64, FP32 = 8, 4
+VARIANT_SCC, VARIANT_KCACHE = 1, 2
+
+# ---------------------------------------------------------------------------
+# cloudsc_params_t  (order == include/cloudsc_amd.h)
+# ---------------------------------------------------------------------------
+PARAM_DOUBLES = (
+    "ptsphy rg rd rcpd retv rlvtt rlstt rlmlt rtt rv "
+    "r2es r3les r3ies r4les r4ies r5les r5ies r5alvcp r5alscp "
+    "ralvdcp ralsdcp ralfdcp rtwat rtice rticecu rtwat_rtice_r rtwat_rticecu_r rkoop1 rkoop2 "
+    "ramid rcldiff rcldiff_convi rclcrit rclcrit_sea rclcrit_land rkconv rprc1 rprc2 "
+    "rcldmax rpecons rvrfactor rprecrhmax rtaumel ramin rlmin rkooptau rcldtopp "
+    "rlcritsnow rsnowlin1 rsnowlin2 ricehi1 ricehi2 riceinit rvice rvrain rvsnow "
+    "rthomo rcovpmin rccn rnice rccnom rccnss rccnsu rcldtopcf rdepliqrefrate "
+    "rdepliqrefdepth rcl_kkaac rcl_kkbac rcl_kkaau rcl_kkbauq rcl_kkbaun "
+    "rcl_kk_cloud_num_sea rcl_kk_cloud_num_land rcl_ai rcl_bi rcl_ci rcl_di "
+    "rcl_x1i rcl_x2i rcl_x3i rcl_x4i rcl_const1i rcl_const2i rcl_const3i rcl_const4i "
+    "rcl_const5i rcl_const6i rcl_apb1 rcl_apb2 rcl_apb3 rcl_as rcl_bs rcl_cs rcl_ds "
+    "rcl_x1s rcl_x2s rcl_x3s rcl_x4s rcl_const1s rcl_const2s rcl_const3s rcl_const4s "
+    "rcl_const5s rcl_const6s rcl_const7s rcl_const8s rdenswat rdensref rcl_ar rcl_br "
+    "rcl_cr rcl_dr rcl_x1r rcl_x2r rcl_x4r rcl_ka273 rcl_cdenom1 rcl_cdenom2 rcl_cdenom3 "
+    "rcl_schmidt rcl_dynvisc rcl_const1r rcl_const2r rcl_const3r rcl_const4r rcl_fac1 "
+    "rcl_fac2 rcl_const5r rcl_const6r rcl_fzrab rcl_fzrbb nshapep nshapeq"
+).split()
+PARAM_INTS = (
+    "lcldextra lcldbudget nssopt ncldtop naeclbc naecldu naeclom naeclss naeclsu nclddiag "
+    "naercld laerliqautolsp laerliqautocp laerliqautocpb laerliqcoll laericesed laericeauto nbeta"
+).split()
+
+
+class Params(C.Structure):
+    _fields_ = [(n, C.c_double) for n in PARAM_DOUBLES] + [(n, C.c_int) for n in PARAM_INTS]
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, float]) -> "Params":
+        p = cls()
+        for n in PARAM_DOUBLES:
+            setattr(p, n, float(d[n]))
+        for n in PARAM_INTS:
+            setattr(p, n, int(d[n]))
+        return p
+
+    def to_dict(self) -> Dict[str, float]:
+        return {n: getattr(self, n) for n in PARAM_DOUBLES + PARAM_INTS}
+
+
+# ---------------------------------------------------------------------------
+# field inventory
+# ---------------------------------------------------------------------------
+# kind: "2d" [lev][klon], "2dh" [lev+1][klon], "3d" [nclv][lev][klon], "1d" [klon]
+INPUT_FIELDS = {
+    "pt": "2d", "pq": "2d", "tendency_tmp_t": "2d", "tendency_tmp_q": "2d", "tendency_tmp_a": "2d",
+    "tendency_tmp_cld": "3d", "pvfl": "2d", "pvfi": "2d", "phrsw": "2d", "phrlw": "2d",
+    "pvervel": "2d", "pap": "2d", "paph": "2dh", "plsm": "1d", "ktype": "1d", "plu": "2d",
+    "psnde": "2d", "pmfu": "2d", "pmfd": "2d", "pa": "2d", "pclv": "3d", "psupsat": "2d",
+}
+AEROSOL_FIELDS = {"plcrit_aer": "2d", "picrit_aer": "2d", "pre_ice": "2d", "pccn": "2d", "pnice": "2d"}
+INOUT_FIELDS = {"plude": "2d"}
+OUTPUT_FIELDS = {
+    "tendency_loc_t": "2d", "tendency_loc_q": "2d", "tendency_loc_a": "2d", "tendency_loc_cld": "3d",
+    "pcovptot": "2d", "prainfrac_toprfz": "1d",
+    "pfsqlf": "2dh", "pfsqif": "2dh", "pfcqnng": "2dh", "pfcqlng": "2dh", "pfsqrf": "2dh",
+    "pfsqsf": "2dh", "pfcqrng": "2dh", "pfcqsng": "2dh", "pfsqltur": "2dh", "pfsqitur": "2dh",
+    "pfplsl": "2dh", "pfplsn": "2dh", "pfhpsl": "2dh", "pfhpsn": "2dh",
+}
+ALL_FIELDS = {**INPUT_FIELDS, **AEROSOL_FIELDS, **INOUT_FIELDS, **OUTPUT_FIELDS}
+
+# The 21 validated fields in the dwarf's print order (cloudsc_validate.c:193-216).
+VALIDATED = [
+    ("PLUDE", "plude"), ("PCOVPTOT", "pcovptot"), ("PRAINFRAC_TOPRFZ", "prainfrac_toprfz"),
+    ("PFSQLF", "pfsqlf"), ("PFSQIF", "pfsqif"), ("PFCQLNG", "pfcqlng"), ("PFCQNNG", "pfcqnng"),
+    ("PFSQRF", "pfsqrf"), ("PFSQSF", "pfsqsf"), ("PFCQRNG", "pfcqrng"), ("PFCQSNG", "pfcqsng"),
+    ("PFSQLTUR", "pfsqltur"), ("PFSQITUR", "pfsqitur"), ("PFPLSL", "pfplsl"), ("PFPLSN", "pfplsn"),
+    ("PFHPSL", "pfhpsl"), ("PFHPSN", "pfhpsn"), ("TENDENCY_LOC%A", "tendency_loc_a"),
+    ("TENDENCY_LOC%Q", "tendency_loc_q"), ("TENDENCY_LOC%T", "tendency_loc_t"),
+    ("TENDENCY_LOC%CLD", "tendency_loc_cld"),
+]
+# Fortran NDIM printed by ERROR_PRINT (VALIDATE_R1/R2/R3)
+VALIDATED_NDIM = {n: (1 if ALL_FIELDS[k] == "1d" else 3 if ALL_FIELDS[k] == "3d" else 2) for n, k in VALIDATED}
+
+class Fields(C.Structure):
+    """cloudsc_fields_t (pointer order == include/cloudsc_amd.h)."""
+    _fields_ = [(n, C.c_void_p) for n in (
+        "pt pq tendency_tmp_t tendency_tmp_q tendency_tmp_a tendency_tmp_cld "
+        "pvfl pvfi phrsw phrlw pvervel pap paph plsm ktype "
+        "plu psnde pmfu pmfd pa pclv psupsat "
+        "plcrit_aer picrit_aer pre_ice pccn pnice plude "
+        "tendency_loc_t tendency_loc_q tendency_loc_a tendency_loc_cld pcovptot prainfrac_toprfz "
+        "pfsqlf pfsqif pfcqnng pfcqlng pfsqrf pfsqsf pfcqrng pfcqsng "
+        "pfsqltur pfsqitur pfplsl pfplsn pfhpsl pfhpsn").split()]
+
+
+class Template(C.Structure):
+    _fields_ = [("klon", C.c_int), ("klev", C.c_int)] + [(n, C.c_void_p) for n in (
+        "pt pq tendency_tmp_t tendency_tmp_q tendency_tmp_a tendency_tmp_cld "
+        "pvfl pvfi phrsw phrlw pvervel pap paph plsm ktype "
+        "plu plude psnde pmfu pmfd pa pclv psupsat "
+        "plcrit_aer picrit_aer pre_ice pccn pnice").split()]
+
+
+class Reference(C.Structure):
+    _fields_ = [("klon", C.c_int), ("klev", C.c_int), ("field", C.c_void_p * 21)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("minval", C.c_double), ("maxval", C.c_double), ("maxerr", C.c_double),
+                ("errsum", C.c_double), ("refsum", C.c_double)]
+
+
+# ---------------------------------------------------------------------------
+# dataset (template) I/O
+# ---------------------------------------------------------------------------
+def field_shape(kind: str, klev: int, klon: int):
+    return {"2d": (klev, klon), "2dh": (klev + 1, klon), "3d": (NCLV, klev, klon), "1d": (klon,)}[kind]
+
+
+def read_params_txt(path: str) -> Dict[str, float]:
+    out: Dict[str, float] = {}
+    with open(path) as fh:
+        for line in fh:
+            line = line.split("#", 1)[0].strip()
+            if not line:
+                continue
+            name, val = line.split("=")
+            name, val = name.strip(), val.strip()
+            out[name] = int(val) if name in PARAM_INTS else float(val)
+    return out
+
+
+def write_params_txt(path: str, params: Dict[str, float]) -> None:
+    with open(path, "w") as fh:
+        fh.write("# CLOUDSC parameter block (YOMCST, YOETHF, TECLDP, PTSPHY); %.17g = exact\n")
+        for n in PARAM_DOUBLES:
+            fh.write("%s = %.17g\n" % (n, params[n]))
+        for n in PARAM_INTS:
+            fh.write("%s = %d\n" % (n, int(params[n])))
+
+
+@dataclass
+class Dataset:
+    """KLON template columns + parameters (+ optional reference outputs)."""
+    klon: int
+    klev: int
+    params: Dict[str, float]
+    inputs: Dict[str, np.ndarray]
+    reference: Dict[str, np.ndarray] = field(default_factory=dict)
+
+    def copy(self) -> "Dataset":
+        return Dataset(self.klon, self.klev, dict(self.params),
+                       {k: v.copy() for k, v in self.inputs.items()},
+                       {k: v.copy() for k, v in self.reference.items()})
+
+
+def load_dataset(path: str = GOLDEN_DIR, with_reference: bool = True) -> Dataset:
+    """Read a raw dataset directory (``input_<NAME>.dat``, ``reference_<NAME>.dat``,
+    ``params.txt``, ``manifest.json``) as written by tools/make_fixtures.py."""
+    man = json.load(open(os.path.join(path, "manifest.json")))
+    klon, klev = man["klon"], man["klev"]
+    params = read_params_txt(os.path.join(path, "params.txt"))
+    inputs = {}
+    for name, kind in {**INPUT_FIELDS, **AEROSOL_FIELDS, **INOUT_FIELDS}.items():
+        fn = os.path.join(path, "input_%s.dat" % name.upper())
+        if not os.path.exists(fn):
+            continue
+        dt = np.int32 if name == "ktype" else np.float64
+        inputs[name] = np.fromfile(fn, dtype=dt).reshape(field_shape(kind, klev, klon))
+    ref = {}
+    if with_reference:
+        for vname, key in VALIDATED:
+            fn = os.path.join(path, "reference_%s.dat" % key.upper())
+            if os.path.exists(fn):
+                ref[key] = np.fromfile(fn, dtype=np.float64).reshape(field_shape(ALL_FIELDS[key], klev, klon))
+    return Dataset(klon, klev, params, inputs, ref)
+
+
+# ---------------------------------------------------------------------------
+# NPROMA-block expansion / contraction (host, numpy)
+# ---------------------------------------------------------------------------
+def nblocks_of(ngptot: int, nproma: int) -> int:
+    return ngptot // nproma + (1 if ngptot % nproma else 0)
+
+
+def global_columns(ngptot: int, nproma: int, col_offset: int = 0) -> np.ndarray:
+    """[nblocks, nproma] global column index of every block lane (lanes past
+    ngptot replicate the map, like the C loader's expand_* which fills them)."""
+    nb = nblocks_of(ngptot, nproma)
+    return col_offset + np.arange(nb * nproma, dtype=np.int64).reshape(nb, nproma)
+
+
+def expand(arr: np.ndarray, kind: str, ngptot: int, nproma: int, col_offset: int = 0,
+           dtype=None) -> np.ndarray:
+    """Template ``[..][klon]`` -> block layout ``[nblocks][..][nproma]`` with g % klon."""
+    klon = arr.shape[-1]
+    src = global_columns(ngptot, nproma, col_offset) % klon            # [nb, nproma]
+    out = np.take(arr, src, axis=-1)                                   # [..., nb, nproma]
+    out = np.moveaxis(out, -2, 0)                                      # [nb, ..., nproma]
+    return np.ascontiguousarray(out, dtype=dtype or arr.dtype)
+
+
+def blocks_to_columns(arr: np.ndarray, ngptot: int) -> np.ndarray:
+    """Block layout ``[nb][..][nproma]`` -> column-last ``[..][ngptot]``."""
+    x = np.moveaxis(arr, 0, -2)                                        # [..., nb, nproma]
+    x = x.reshape(x.shape[:-2] + (-1,))
+    return x[..., :ngptot]
+
+
+@dataclass
+class HostState:
+    """All kernel fields in block layout on the host (used with the oracle)."""
+    ngptot: int
+    nproma: int
+    klev: int
+    precision: int
+    arrays: Dict[str, np.ndarray]
+
+    def fields(self) -> Fields:
+        f = Fields()
+        for name, _ in Fields._fields_:
+            a = self.arrays.get(name)
+            setattr(f, name, a.ctypes.data if a is not None else None)
+        return f
+
+
+def make_host_state(ds: Dataset, ngptot: int, nproma: int, precision: int = FP64,
+                    col_offset: int = 0) -> HostState:
+    real = np.float64 if precision == FP64 else np.float32
+    nb = nblocks_of(ngptot, nproma)
+    arrays = {}
+    for name, arr in ds.inputs.items():
+        kind = ALL_FIELDS[name]
+        arrays[name] = expand(arr, kind, ngptot, nproma, col_offset,
+                              dtype=np.int32 if name == "ktype" else real)
+    for name, kind in OUTPUT_FIELDS.items():
+        shp = (nb,) + field_shape(kind, ds.klev, nproma)
+        arrays[name] = np.full(shp, np.nan, dtype=real)                # callee must write all
+    return HostState(ngptot, nproma, ds.klev, precision, arrays)
+
+
+# ---------------------------------------------------------------------------
+# validation (Fortran ERROR_PRINT semantics, validate_mod.F90:118-296)
+# ---------------------------------------------------------------------------
+def field_stats(field: np.ndarray, ref: np.ndarray) -> tuple:
+    f = field.astype(np.float64).ravel()
+    r = ref.astype(np.float64).ravel()
+    d = np.abs(f - r)
+    return (float(f.min()), float(f.max()), float(d.max()), float(d.sum()), float(np.abs(r).sum()))
+
+
+def rel_error(errsum: float, refsum: float, eps: float = np.finfo(np.float64).eps):
+    """(zrelerr, iopt) exactly as ERROR_PRINT (validate_mod.F90:273-283)."""
+    if errsum < eps:
+        return 0.0, 1
+    if refsum < eps:
+        return errsum / (1.0 + refsum), 2
+    return errsum / refsum, 3
+
+
+def format_row(name: str, ndim: int, st: tuple, ngptot: int, eps: float = np.finfo(np.float64).eps) -> str:
+    mn, mx, maxerr, errsum, refsum = st
+    rel, iopt = rel_error(errsum, refsum, eps)
+    warn = " !!!!" if rel > 10.0 * eps else "     "
+    # Fortran format (1X,A20,1X,I1,'D',I1,5(1X,E20.13),A)
+    return " %20s %dD%d %20.13E %20.13E %20.13E %20.13E %20.13E%s" % (
+        name, ndim, iopt, mn, mx, maxerr, errsum / ngptot, 100.0 * rel, warn)
+
+
+def state_outputs_to_template(arrays: Dict[str, np.ndarray], ngptot: int) -> Dict[str, np.ndarray]:
+    return {k: blocks_to_columns(arrays[k], ngptot) for _, k in VALIDATED}
+
+
+# ---------------------------------------------------------------------------
+# GPU library (no fallback)
+# ---------------------------------------------------------------------------
+class CloudscError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def gpu_lib(path: Optional[str] = None):
+    """Load libcloudsc_amd.so.  Raises if it is missing: there is no CPU fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("CLOUDSC_AMD_LIB", LIB_PATH)
+    if not os.path.exists(path):
+        raise CloudscError("libcloudsc_amd.so not built (%s): run __graft_entry__.build()" % path)
+    lib = C.CDLL(path)
+    lib.cloudsc_strerror.restype = C.c_char_p
+    lib.cloudsc_last_hip_error.restype = C.c_char_p
+    lib.cloudsc_abi_sizeof.restype = C.c_longlong
+    lib.cloudsc_gpu_scratch_bytes.restype = C.c_longlong
+    lib.cloudsc_state_field_elems.restype = C.c_longlong
+    lib.cloudsc_state_create.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_longlong, C.POINTER(Template), C.POINTER(Params)]
+    lib.cloudsc_state_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]
+    lib.cloudsc_state_validate.argtypes = [C.c_void_p, C.POINTER(Reference), C.POINTER(Stats)]
+    lib.cloudsc_state_download.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    lib.cloudsc_state_field_elems.argtypes = [C.c_void_p, C.c_int]
+    lib.cloudsc_state_destroy.argtypes = [C.c_void_p]
+    lib.cloudsc_state_sync.argtypes = [C.c_void_p]
+    lib.cloudsc_state_reset.argtypes = [C.c_void_p]
+    lib.cloudsc_state_fields.argtypes = [C.c_void_p, C.POINTER(Fields)]
+    lib.cloudsc_gpu_init.argtypes = [C.c_int, C.POINTER(Params)]
+    lib.cloudsc_gpu_run.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.POINTER(Fields), C.c_void_p]
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        lib = gpu_lib()
+        raise CloudscError("cloudsc error %d: %s (hip: %s)" % (
+            rc, lib.cloudsc_strerror(rc).decode(), (lib.cloudsc_last_hip_error() or b"").decode()))
+
+
+def make_template(ds: Dataset, keep: list) -> Template:
+    t = Template()
+    t.klon, t.klev = ds.klon, ds.klev
+    for name, _ in Template._fields_[2:]:
+        a = ds.inputs.get(name)
+        if a is not None:
+            a = np.ascontiguousarray(a)
+            keep.append(a)
+            setattr(t, name, a.ctypes.data)
+    return t
+
+
+def make_reference(ds: Dataset, keep: list) -> Reference:
+    r = Reference()
+    r.klon, r.klev = ds.klon, ds.klev
+    for i, (_, key) in enumerate(VALIDATED):
+        a = np.ascontiguousarray(ds.reference[key], dtype=np.float64)
+        keep.append(a)
+        r.field[i] = a.ctypes.data
+    return r
+
+
+class GpuState:
+    """Device-resident CLOUDSC problem (cloudsc_state_* of cloudsc_amd.h)."""
+
+    def __init__(self, ds: Dataset, ngptot: int, nproma: int = 128, precision: int = FP64,
+                 device: int = 0, col_offset: int = 0):
+        self.lib = gpu_lib()
+        self.ds, self.ngptot, self.nproma, self.precision = ds, ngptot, nproma, precision
+        keep: list = []
+        tmpl = make_template(ds, keep)
+        self._params = Params.from_dict(ds.params)
+        h = C.c_void_p()
+        check(self.lib.cloudsc_state_create(C.byref(h), device, precision, ngptot, nproma,
+                                            col_offset, C.byref(tmpl), C.byref(self._params)))
+        self.h = h
+
+    def run(self, variant: int = VARIANT_KCACHE, reps: int = 1) -> np.ndarray:
+        ms = (C.c_float * reps)()
+        check(self.lib.cloudsc_state_run(self.h, variant, reps, ms))
+        return np.array(ms[:], dtype=np.float64)
+
+    def sync(self) -> None:
+        check(self.lib.cloudsc_state_sync(self.h))
+
+    def reset(self) -> None:
+        check(self.lib.cloudsc_state_reset(self.h))
+
+    def validate(self, ds: Optional[Dataset] = None) -> list:
+        ds = ds or self.ds
+        keep: list = []
+        ref = make_reference(ds, keep)
+        st = (Stats * 21)()
+        check(self.lib.cloudsc_state_validate(self.h, C.byref(ref), st))
+        return [(s.minval, s.maxval, s.maxerr, s.errsum, s.refsum) for s in st]
+
+    def download(self, key: str) -> np.ndarray:
+        idx = [k for _, k in VALIDATED].index(key)
+        n = self.lib.cloudsc_state_field_elems(self.h, idx)
+        out = np.empty(n, dtype=np.float64)
+        check(self.lib.cloudsc_state_download(self.h, idx, out.ctypes.data))
+        nb = nblocks_of(self.ngptot, self.nproma)
+        return out.reshape((nb,) + field_shape(ALL_FIELDS[key], self.ds.klev, self.nproma))
+
+    def outputs(self) -> Dict[str, np.ndarray]:
+        """All 21 validated fields, column-last template-like order [..][ngptot]."""
+        return {k: blocks_to_columns(self.download(k), self.ngptot) for _, k in VALIDATED}
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.cloudsc_state_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

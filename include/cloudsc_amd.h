@@ -1,0 +1,241 @@
+/*
+ * cloudsc_amd.h -- C ABI of the MI355X-native CLOUDSC dwarf (libcloudsc_amd.so).
+ *
+ * Plain C: no C++ or torch types, plain pointers and sizes.  Every entry point
+ * returns 0 on success or a negative CLOUDSC_E* code; the library never calls
+ * exit().  State is per device (no mutable process globals), so one host thread
+ * per device -- or one thread driving N devices -- is safe.
+ *
+ * Which reference interface each declaration replaces (paths relative to the
+ * lukasm91/dwarf-p-cloudsc checkout):
+ *
+ *   cloudsc_params_t   <- struct TECLDP (src/cloudsc_c/cloudsc/yoecldp_c.h:21-141)
+ *                         + YOMCST globals (yomcst_c.h:14-72) + YOETHF globals
+ *                         (yoethf_c.h:14-36) + PTSPHY, filled by load_state()
+ *                         (src/cloudsc_c/cloudsc/load_state.c:538-690)
+ *   cloudsc_fields_t   <- the 56 array arguments of cloudsc_c()
+ *                         (src/cloudsc_c/cloudsc/cloudsc_c.h:18-29) and of the
+ *                         CUDA kernel (src/cloudsc_cuda/cloudsc/cloudsc_c_k_caching.cu:13-40)
+ *   cloudsc_gpu_init   <- cudaMemcpy of the TECLDP struct + the 28 by-value
+ *                         constants (src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:383,412-416)
+ *   cloudsc_gpu_run    <- cloudsc_c<<<grid,nproma>>>(...) (cloudsc_driver.cu:391-416)
+ *                         and, for the CPU dwarf, the OpenMP block loop calling
+ *                         cloudsc_c() (src/cloudsc_c/cloudsc/cloudsc_driver.c:183-217)
+ *   cloudsc_gpu_state_* <- the driver plumbing around the kernel: load+expand
+ *                         (load_state.c:69-184,279), timing (cloudsc_driver.c:181-262),
+ *                         validation (src/common/module/validate_mod.F90:118-296)
+ *
+ * Field layout (identical to the reference C/CUDA drivers, cloudsc_driver.c:114-171):
+ * NPROMA-blocked, nblocks = ceil(ngptot/nproma), column jl of block b is global
+ * column b*nproma+jl.
+ *   full-level field     [nblocks][klev][nproma]
+ *   half-level field     [nblocks][klev+1][nproma]      (paph, the 14 flux fields)
+ *   species field        [nblocks][NCLV][klev][nproma]  (pclv, tendency_*_cld)
+ *   surface field        [nblocks][nproma]              (plsm, ktype, prainfrac_toprfz)
+ * Element type is double for CLOUDSC_FP64 and float for CLOUDSC_FP32 (ktype is
+ * always int32).  Lanes jl >= bsize of the last block are never read or written.
+ *
+ * Output contract (stronger than the reference C kernel, matches the CUDA one):
+ * the callee writes EVERY output element of every active column -- including
+ * tendency_loc_cld[vapour] (zero) and pcovptot at levels < NCLDTOP (zero) --
+ * so the caller need not pre-zero (cf. cloudsc_driver.c:199-200).  plude is
+ * read-modify-write exactly as in the reference (cloudsc_c.c:970,980).
+ */
+#ifndef CLOUDSC_AMD_H
+#define CLOUDSC_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLOUDSC_NCLV 5          /* ql, qi, qr, qs, qv (yoecldp_c.h:13-18)            */
+#define CLOUDSC_MAX_KLEV 256    /* kernels keep the column in registers: no klev cap  */
+                                /* other than the carried-state size; checked on entry */
+
+/* precision selector */
+#define CLOUDSC_FP64 8
+#define CLOUDSC_FP32 4
+
+/* kernel variant selector */
+#define CLOUDSC_VARIANT_SCC    1   /* SCC baseline: level phases as separate sweeps, temporaries in HBM scratch */
+#define CLOUDSC_VARIANT_KCACHE 2   /* SCC-k-caching: one fused level loop, carried state in registers       */
+
+/* error codes */
+#define CLOUDSC_OK            0
+#define CLOUDSC_EINVAL      (-1)   /* bad argument (sizes, NULL pointer, precision, variant) */
+#define CLOUDSC_ENODEV      (-2)   /* no such HIP device                                      */
+#define CLOUDSC_EHIP        (-3)   /* a HIP runtime call failed (see cloudsc_last_hip_error) */
+#define CLOUDSC_ENOINIT     (-4)   /* cloudsc_gpu_init not called for this device           */
+#define CLOUDSC_ENOMEM      (-5)   /* device or host allocation failed                        */
+#define CLOUDSC_EIO         (-6)   /* file could not be read / wrong format                   */
+
+/* ------------------------------------------------------------------------ */
+/* Parameters: YOMCST + YOETHF + TECLDP (without rbeta/rbetap1) + PTSPHY     */
+/* ------------------------------------------------------------------------ */
+typedef struct cloudsc_params {
+  double ptsphy;
+  /* YOMCST (the 9 the kernel reads) */
+  double rg, rd, rcpd, retv, rlvtt, rlstt, rlmlt, rtt, rv;
+  /* YOETHF */
+  double r2es, r3les, r3ies, r4les, r4ies, r5les, r5ies, r5alvcp, r5alscp;
+  double ralvdcp, ralsdcp, ralfdcp, rtwat, rtice, rticecu, rtwat_rtice_r, rtwat_rticecu_r;
+  double rkoop1, rkoop2;
+  /* TECLDP doubles, in yoecldp_c.h order */
+  double ramid, rcldiff, rcldiff_convi, rclcrit, rclcrit_sea, rclcrit_land, rkconv, rprc1, rprc2;
+  double rcldmax, rpecons, rvrfactor, rprecrhmax, rtaumel, ramin, rlmin, rkooptau, rcldtopp;
+  double rlcritsnow, rsnowlin1, rsnowlin2, ricehi1, ricehi2, riceinit, rvice, rvrain, rvsnow;
+  double rthomo, rcovpmin, rccn, rnice, rccnom, rccnss, rccnsu, rcldtopcf, rdepliqrefrate;
+  double rdepliqrefdepth, rcl_kkaac, rcl_kkbac, rcl_kkaau, rcl_kkbauq, rcl_kkbaun;
+  double rcl_kk_cloud_num_sea, rcl_kk_cloud_num_land, rcl_ai, rcl_bi, rcl_ci, rcl_di;
+  double rcl_x1i, rcl_x2i, rcl_x3i, rcl_x4i, rcl_const1i, rcl_const2i, rcl_const3i, rcl_const4i;
+  double rcl_const5i, rcl_const6i, rcl_apb1, rcl_apb2, rcl_apb3, rcl_as, rcl_bs, rcl_cs, rcl_ds;
+  double rcl_x1s, rcl_x2s, rcl_x3s, rcl_x4s, rcl_const1s, rcl_const2s, rcl_const3s, rcl_const4s;
+  double rcl_const5s, rcl_const6s, rcl_const7s, rcl_const8s, rdenswat, rdensref, rcl_ar, rcl_br;
+  double rcl_cr, rcl_dr, rcl_x1r, rcl_x2r, rcl_x4r, rcl_ka273, rcl_cdenom1, rcl_cdenom2, rcl_cdenom3;
+  double rcl_schmidt, rcl_dynvisc, rcl_const1r, rcl_const2r, rcl_const3r, rcl_const4r, rcl_fac1;
+  double rcl_fac2, rcl_const5r, rcl_const6r, rcl_fzrab, rcl_fzrbb, nshapep, nshapeq;
+  /* TECLDP integers / logicals (logical: 0 = .FALSE., nonzero = .TRUE.) */
+  int lcldextra, lcldbudget, nssopt, ncldtop;
+  int naeclbc, naecldu, naeclom, naeclss, naeclsu, nclddiag, naercld;
+  int laerliqautolsp, laerliqautocp, laerliqautocpb, laerliqcoll, laericesed, laericeauto;
+  int nbeta;
+} cloudsc_params_t;
+
+/* ------------------------------------------------------------------------ */
+/* Field pointers (device pointers for cloudsc_gpu_run)                      */
+/* ------------------------------------------------------------------------ */
+typedef struct cloudsc_fields {
+  /* inputs */
+  const void *pt, *pq;
+  const void *tendency_tmp_t, *tendency_tmp_q, *tendency_tmp_a, *tendency_tmp_cld;
+  const void *pvfl, *pvfi, *phrsw, *phrlw, *pvervel, *pap, *paph, *plsm;
+  const int  *ktype;
+  const void *plu, *psnde, *pmfu, *pmfd, *pa, *pclv, *psupsat;
+  /* aerosol inputs: read only when the matching LAER* flag is set; may be NULL otherwise */
+  const void *plcrit_aer, *picrit_aer, *pre_ice, *pccn, *pnice;
+  /* in/out */
+  void *plude;
+  /* outputs */
+  void *tendency_loc_t, *tendency_loc_q, *tendency_loc_a, *tendency_loc_cld;
+  void *pcovptot, *prainfrac_toprfz;
+  void *pfsqlf, *pfsqif, *pfcqnng, *pfcqlng, *pfsqrf, *pfsqsf, *pfcqrng, *pfcqsng;
+  void *pfsqltur, *pfsqitur, *pfplsl, *pfplsn, *pfhpsl, *pfhpsn;
+} cloudsc_fields_t;
+
+/* ------------------------------------------------------------------------ */
+/* Low-level boundary: run the kernel on caller-owned device buffers         */
+/* ------------------------------------------------------------------------ */
+
+/* Number of visible HIP devices. */
+int cloudsc_gpu_device_count(int *count);
+
+/* Copy the parameter block into the device's __constant__ mirrors (fp64 and
+ * fp32).  Must be called once per device before cloudsc_gpu_run. */
+int cloudsc_gpu_init(int device, const cloudsc_params_t *params);
+
+/* Enqueue one CLOUDSC step over ngptot columns on `stream` (a hipStream_t, or
+ * NULL for the default stream) of `device`.  Asynchronous; errors in the launch
+ * configuration are returned, asynchronous faults surface at the caller's sync.
+ * SCC needs a workspace: pass scratch of cloudsc_gpu_scratch_bytes() bytes (or
+ * NULL for KCACHE). */
+int cloudsc_gpu_run(int device, void *stream, int precision, int variant,
+                    int ngptot, int nproma, int klev,
+                    const cloudsc_fields_t *device_fields, void *scratch);
+
+/* Bytes of device scratch the SCC variant needs for (ngptot, nproma, klev, precision). */
+long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev);
+
+/* Human-readable message for an error code; last HIP error string of this thread. */
+const char *cloudsc_strerror(int code);
+const char *cloudsc_last_hip_error(void);
+
+/* ABI introspection for bindings: sizeof of the public structs
+ * (0 params, 1 fields, 2 template, 3 reference, 4 stats), -1 otherwise. */
+long long cloudsc_abi_sizeof(int which);
+
+/* ------------------------------------------------------------------------ */
+/* Dwarf plumbing on the device: expand a KLON-column template to NGPTOT      */
+/* columns (global column g -> template column g % klon, load_state.c:69-184, */
+/* expand_mod.F90:173-200), run, time, and validate against a KLON-column     */
+/* reference with the Fortran ERROR_PRINT statistics (validate_mod.F90:263). */
+/* ------------------------------------------------------------------------ */
+
+/* Template / reference arrays in the HDF5 / Serialbox order: [lev][klon],
+ * species [nclv][lev][klon], surface [klon].  Always double (fp32 runs convert
+ * at expansion, as file_io_mod.F90:96-112 does). */
+typedef struct cloudsc_template {
+  int klon, klev;
+  const double *pt, *pq, *tendency_tmp_t, *tendency_tmp_q, *tendency_tmp_a, *tendency_tmp_cld;
+  const double *pvfl, *pvfi, *phrsw, *phrlw, *pvervel, *pap, *paph, *plsm;
+  const int    *ktype;
+  const double *plu, *plude, *psnde, *pmfu, *pmfd, *pa, *pclv, *psupsat;
+  const double *plcrit_aer, *picrit_aer, *pre_ice, *pccn, *pnice;   /* may be NULL */
+} cloudsc_template_t;
+
+/* The 21 validated fields, in the dwarf's print order (cloudsc_validate.c:193-216). */
+#define CLOUDSC_NVALID 21
+enum cloudsc_field_id {
+  CLOUDSC_F_PLUDE = 0, CLOUDSC_F_PCOVPTOT, CLOUDSC_F_PRAINFRAC_TOPRFZ,
+  CLOUDSC_F_PFSQLF, CLOUDSC_F_PFSQIF, CLOUDSC_F_PFCQLNG, CLOUDSC_F_PFCQNNG,
+  CLOUDSC_F_PFSQRF, CLOUDSC_F_PFSQSF, CLOUDSC_F_PFCQRNG, CLOUDSC_F_PFCQSNG,
+  CLOUDSC_F_PFSQLTUR, CLOUDSC_F_PFSQITUR, CLOUDSC_F_PFPLSL, CLOUDSC_F_PFPLSN,
+  CLOUDSC_F_PFHPSL, CLOUDSC_F_PFHPSN, CLOUDSC_F_TENDENCY_LOC_A,
+  CLOUDSC_F_TENDENCY_LOC_Q, CLOUDSC_F_TENDENCY_LOC_T, CLOUDSC_F_TENDENCY_LOC_CLD
+};
+
+/* Reference outputs for the KLON template columns, same order as the enum;
+ * each array in template order ([lev][klon], [nclv][lev][klon] or [klon]). */
+typedef struct cloudsc_reference {
+  int klon, klev;
+  const double *field[CLOUDSC_NVALID];
+} cloudsc_reference_t;
+
+/* Per-field statistics, the inputs of ERROR_PRINT (validate_mod.F90:263-296). */
+typedef struct cloudsc_stats {
+  double minval, maxval, maxerr, errsum, refsum;
+} cloudsc_stats_t;
+
+typedef struct cloudsc_gpu_state cloudsc_gpu_state_t;
+
+/* Allocate device buffers for columns [col_offset, col_offset+ngptot) of the
+ * global problem and expand the template into them on the device (g % klon
+ * with g the GLOBAL column index, so a sharded run is bit-identical to an
+ * unsharded one).  Keeps a pristine copy of plude for repeated runs. */
+int cloudsc_state_create(cloudsc_gpu_state_t **state, int device, int precision,
+                         int ngptot, int nproma, long long col_offset,
+                         const cloudsc_template_t *tmpl, const cloudsc_params_t *params);
+
+/* Device pointers of the state's buffers (block layout) -- for callers that
+ * want to drive cloudsc_gpu_run themselves. */
+int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out);
+
+/* Restore plude from the pristine copy (outside any timed region). */
+int cloudsc_state_reset(cloudsc_gpu_state_t *state);
+
+/* Launch `reps` back-to-back steps of `variant` on the state's stream and
+ * time each with HIP events recorded on that stream.  plude is restored
+ * before every step by a device copy that is NOT inside the event pair.
+ * ms_per_step[reps] receives the per-step kernel time (may be NULL). */
+int cloudsc_state_run(cloudsc_gpu_state_t *state, int variant, int reps, float *ms_per_step);
+
+/* Wait for all work of the state's stream. */
+int cloudsc_state_sync(cloudsc_gpu_state_t *state);
+
+/* Field-wise statistics vs a KLON-column reference, computed on the device
+ * (modulo indexing; no expanded reference in host or device memory). */
+int cloudsc_state_validate(cloudsc_gpu_state_t *state, const cloudsc_reference_t *ref,
+                           cloudsc_stats_t stats[CLOUDSC_NVALID]);
+
+/* Copy one validated output field to host memory in BLOCK layout as doubles
+ * (fp32 states are widened).  `host` must hold the field's blocked size. */
+int cloudsc_state_download(cloudsc_gpu_state_t *state, int field_id, double *host);
+
+/* Element count of a validated field in block layout for this state. */
+long long cloudsc_state_field_elems(const cloudsc_gpu_state_t *state, int field_id);
+
+int cloudsc_state_destroy(cloudsc_gpu_state_t *state);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLOUDSC_AMD_H */

@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/ (run in the build
+container, where /root/reference exists; the GPU box only reads the result).
+
+1. tests/golden/cloudsc100/  -- the reference's own 100-column data set:
+   * input_<FIELD>.dat     raw little-endian arrays copied byte-for-byte from
+                           data/input_<FIELD>.dat (Serialbox binary; C order
+                           [lev][klon] / [nclv][lev][klon] / [klon], i.e. the
+                           HDF5 dataset layout, serialbox2hdf5/serialbox2hdf5.py:11-33)
+   * reference_<FIELD>.dat the 21 golden outputs, data/reference_<FIELD>.dat
+                           (byte-identical to config-files/reference.h5)
+   * params.txt            PTSPHY + YOMCST + YOETHF + YRECLDP scalars from
+                           data/MetaData-input.json global_meta_info (%.17g)
+   * manifest.json         klon, klev, field list
+2. tests/golden/scenario_{W,M}.npz -- perturbed inputs that reach the branches the
+   shipped data never exercises (rain, melting, freezing, land),
+   with the outputs of the UNMODIFIED reference kernel (oracle/_ref) as expected
+   values.  Inputs and outputs are both stored: RNG draw order is not relied on.
+"""
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "dwarf-p-cloudsc_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import cloudsc_amd as ca  # noqa: E402
+
+REFDATA = "/root/reference/data"
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def json_params(meta_path):
+    g = json.load(open(meta_path))["global_meta_info"]
+    p = {}
+    for k, v in g.items():
+        name = k.lower()
+        if name.startswith("yrecldp_"):
+            name = name[len("yrecldp_"):]
+        p[name] = v["value"]
+    out = {}
+    for n in ca.PARAM_DOUBLES:
+        out[n] = float(p[n])
+    for n in ca.PARAM_INTS:
+        out[n] = int(p[n])
+    return out, g["KLON"]["value"], g["KLEV"]["value"]
+
+
+def make_cloudsc100():
+    d = os.path.join(OUT, "cloudsc100")
+    os.makedirs(d, exist_ok=True)
+    params, klon, klev = json_params(os.path.join(REFDATA, "MetaData-input.json"))
+    ca.write_params_txt(os.path.join(d, "params.txt"), params)
+    names = list(ca.INPUT_FIELDS) + list(ca.INOUT_FIELDS) + ["picrit_aer", "pre_ice", "pnice"]
+    for n in names:
+        shutil.copyfile(os.path.join(REFDATA, "input_%s.dat" % n.upper()),
+                        os.path.join(d, "input_%s.dat" % n.upper()))
+    for _, key in ca.VALIDATED:
+        shutil.copyfile(os.path.join(REFDATA, "reference_%s.dat" % key.upper()),
+                        os.path.join(d, "reference_%s.dat" % key.upper()))
+    json.dump({"klon": klon, "klev": klev, "source": "lukasm91/dwarf-p-cloudsc data/ (Serialbox raw)",
+               "inputs": sorted(n.upper() for n in names),
+               "reference": [k.upper() for _, k in ca.VALIDATED]},
+              open(os.path.join(d, "manifest.json"), "w"), indent=1)
+    print("wrote", d)
+
+
+PERTURBED = ["pt", "pq", "pclv", "plsm"]
+
+
+def scenario(ds, name):
+    """SURVEY.md §8c recipes, seed 20250227."""
+    s = ds.copy()
+    rng = np.random.default_rng(20250227)
+    klev, klon = s.klev, s.klon
+    if name == "W":     # warm: rain autoconversion/evaporation, melting, land
+        s.inputs["pt"] = s.inputs["pt"] + 25.0 + rng.uniform(-2.0, 2.0, size=(klev, klon))
+    elif name == "M":   # mixed: melting layer -> rain freezing, homogeneous freezing
+        pt = s.inputs["pt"].copy()
+        bump = 1.6 * np.linspace(0.0, 22.0, 30) * np.sin(np.linspace(0.0, np.pi, 30))
+        pt[95:125, :] += bump[:, None] + rng.uniform(-1.0, 1.0, size=(30, klon))
+        s.inputs["pt"] = pt
+        pclv = s.inputs["pclv"].copy()
+        pclv[2, 100:137, :] += 2e-5
+        cold = pt < 233.0
+        pclv[0][cold] += 1e-5
+        s.inputs["pclv"] = pclv
+        pq = s.inputs["pq"].copy()
+        pq[pt < 235.0] *= 1.6
+        s.inputs["pq"] = pq
+    plsm = s.inputs["plsm"].copy()
+    plsm[1::2] = 1.0
+    s.inputs["plsm"] = plsm
+    return s
+
+
+def make_scenarios():
+    import oracle  # the compiled reference kernel (oracle/_ref)
+    if not oracle.ref_available():
+        raise SystemExit("oracle/_ref/libcloudsc_ref.so missing: make -C oracle")
+    ds = ca.load_dataset(os.path.join(OUT, "cloudsc100"))
+    for name in ("W", "M"):
+        s = scenario(ds, name)
+        st, _ = oracle.run_ref(s, s.klon, s.klon, nthreads=1)
+        outs = ca.state_outputs_to_template(st.arrays, s.klon)
+        arrays = {"in_" + k: s.inputs[k] for k in PERTURBED}
+        arrays.update({"out_" + k: v for k, v in outs.items()})
+        for k, v in outs.items():
+            assert np.all(np.isfinite(v)), (name, k)
+        fn = os.path.join(OUT, "scenario_%s.npz" % name)
+        np.savez_compressed(fn, **arrays)
+        print("wrote", fn, "rain tendency nonzero points:",
+              int(np.count_nonzero(outs["tendency_loc_cld"][2])),
+              "prainfrac>0 columns:", int(np.count_nonzero(outs["prainfrac_toprfz"])))
+
+
+def load_scenario(name, base=None):
+    """Dataset with the scenario's perturbed inputs and reference outputs."""
+    base = base or ca.load_dataset(os.path.join(OUT, "cloudsc100"))
+    z = np.load(os.path.join(OUT, "scenario_%s.npz" % name))
+    s = base.copy()
+    for k in z.files:
+        if k.startswith("in_"):
+            s.inputs[k[3:]] = z[k]
+    s.reference = {k[4:]: z[k] for k in z.files if k.startswith("out_")}
+    return s
+
+
+if __name__ == "__main__":
+    make_cloudsc100()
+    make_scenarios()
