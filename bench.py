@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""CLOUDSC dwarf benchmark: grid-columns/sec at NGPTOT=163840 per GPU, KLEV=137,
+fp64 (BASELINE.json metric), plus the HBM roofline of the k-caching kernel and
+the CPU baseline measured on this box's host cores.
+
+One process per GPU (launched by torch.distributed.run for N>1).  Columns shard
+with NO data-path collective: rank r owns global columns
+[r*NGPTOT, (r+1)*NGPTOT) (weak scaling, the g % 100 map of the GLOBAL index, so
+a sharded run is bit-identical to an unsharded one).  torch.distributed (gloo)
+is used only for the barrier around the timed region and the max-over-ranks.
+
+A "step" = one CLOUDSC pass over the rank's NGPTOT resident columns: restore of
+the INOUT field plude (device copy, cloudsc_c.c:970,980) + one kernel launch.
+The timed region brackets exactly K steps with barrier + device sync on both
+sides; value = all columns of all ranks / max-over-ranks wall time.  The kernel
+alone is also timed with HIP events recorded on the launch stream
+(roofline.achieved uses that kernel time).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "dwarf-p-cloudsc_amd"))
+
+BYTES_PER_COL = {8: 56036, 4: 28020}     # SURVEY.md §8d algorithmic bytes per column
+HBM_PEAK_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--ngptot", type=int, default=163840, help="columns per GPU")
+    p.add_argument("--nproma", type=int, default=128)
+    p.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
+    p.add_argument("--variant", choices=["kcache", "scc"], default="kcache")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=65536, help="columns in the CPU baseline sample")
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                   help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
+    return p.parse_args()
+
+
+def cpu_baseline(ds, ncols, nproma=32):
+    """Reference C kernel (oracle/_ref, compiled from the reference sources) when
+    present, else the oracle restatement; OpenMP over NPROMA blocks on the host
+    cores (cloudsc_driver.c:183-217).  Returns the cpu_baseline object."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    kind = "reference" if oracle.ref_available() else "port"
+    best = None
+    for _ in range(2):
+        if kind == "reference":
+            _, secs = oracle.run_ref(ds, ncols, nproma, nthreads=nthreads)
+        else:
+            _, secs = oracle.run_oracle(ds, ncols, nproma, nthreads=nthreads)
+        best = secs if best is None else min(best, secs)
+    return {"value": ncols / best, "unit": "columns/s", "cores": nthreads, "kind": kind,
+            "sample": "%d columns of the same fp64 workload (g %% 100 expansion, KLEV=137), NPROMA=%d, "
+                      "%d OpenMP threads, best of 2 block loops (%s)" % (
+                          ncols, nproma, nthreads,
+                          "src/cloudsc_c/cloudsc/cloudsc_c.c" if kind == "reference" else "oracle/cloudsc_oracle.c")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import cloudsc_amd as ca
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    prec = ca.FP64 if args.precision == "fp64" else ca.FP32
+    variant = ca.VARIANT_KCACHE if args.variant == "kcache" else ca.VARIANT_SCC
+    ds = ca.load_dataset()
+    g = ca.GpuState(ds, args.ngptot, args.nproma, prec, device=local_rank,
+                    col_offset=rank * args.ngptot)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    if args.warmup > 0:
+        g.run(variant, args.warmup)
+    barrier()
+    g.sync()
+    t0 = time.perf_counter()
+    kernel_ms = g.run(variant, args.steps)      # plude restore + launch per step; events around launch
+    g.sync()
+    t1 = time.perf_counter()
+    barrier()
+    wall = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    # validation of the last step against reference.h5 (device-side statistics)
+    stats = g.validate()
+    worst = 0.0
+    for (mn, mx, maxerr, errsum, refsum) in stats:
+        worst = max(worst, errsum / refsum if refsum > 0 else errsum)
+    g.close()
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    total_cols = args.ngptot * world
+    ms_per_step = 1e3 * wall / args.steps
+    value = total_cols * args.steps / wall
+    k_avg_ms = float(np.mean(kernel_ms))
+    bpc = BYTES_PER_COL[prec]
+    achieved = bpc * args.ngptot / (k_avg_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            key = "%s_%s_%d_%d" % (args.variant, args.precision, args.ngptot, args.nproma)
+            if key in tj:
+                traffic = tj[key]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+    line = {
+        "metric": "grid-columns/sec at NGPTOT=163840 KLEV=137 fp64; achieved HBM GB/s vs peak",
+        "value": round(value, 1),
+        "unit": "columns/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64" if prec == ca.FP64 else "f32",
+        "data": "reference 100-column IFS state (tests/golden/cloudsc100, from the reference's data/) "
+                "expanded on the device with g % 100",
+        "config": {"workload": "CLOUDSC %s, NGPTOT=%d per GPU, KLEV=%d, NPROMA=%d, %s" % (
+            "SCC-k-caching" if variant == ca.VARIANT_KCACHE else "SCC (HBM temporaries)",
+            args.ngptot, ds.klev, args.nproma, args.precision),
+            "ngptot_per_gpu": args.ngptot, "ngptot_total": total_cols, "klev": ds.klev,
+            "nproma": args.nproma, "variant": args.variant, "parallelism": "columns sharded, %d GPU(s)" % world},
+        "kernel_ms": round(k_avg_ms, 4),
+        "kernel_ms_min": round(float(np.min(kernel_ms)), 4),
+        "validation_worst_rel_l1": worst,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_column": bpc},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(ds, min(args.cpu_sample, args.ngptot))
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,91 @@
+// cloudsc_dev.h -- device-side parameter block and thermodynamic helpers shared
+// by the CLOUDSC kernels (k-caching and SCC) for CDNA4 / gfx950.
+//
+// The YOMCST / YOETHF constants and the TECLDP tuning parameters the kernel
+// reads (reference: src/cloudsc_c/cloudsc/{yomcst_c,yoethf_c,yoecldp_c}.h) live
+// in __constant__ memory, one mirror per precision; uniform across the grid,
+// so every access is a scalar (s_load) read.  A few derived constants that the
+// reference recomputes per point (1/PTSPHY, RD/RCPD, 1/(PTSPHY*RG), ...) are
+// folded on the host with the SAME IEEE operation, so results do not change.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace cloudsc {
+
+template <typename real>
+struct DevParams {
+  // YOMCST / YOETHF
+  real ptsphy, rg, rd, retv, rlvtt, rlstt, rtt, rv;
+  real r2es, r3les, r3ies, r4les, r4ies, r5les, r5ies, r5alvcp, r5alscp;
+  real ralvdcp, ralsdcp, ralfdcp, rtwat, rtice, rtwat_rtice_r, rkoop1, rkoop2;
+  // TECLDP (subset the kernel reads)
+  real ramid, rprecrhmax, rtaumel, ramin, rlmin, rlcritsnow, rsnowlin2;
+  real riceinit, rvice, rvrain, rvsnow, rthomo, rcovpmin, rnice, rcldtopcf, rdepliqrefrate;
+  real rdepliqrefdepth, rvrfactor, rclcrit_sea, rclcrit_land;
+  real rcl_kkaac, rcl_kkbac, rcl_kkaau, rcl_kkbauq, rcl_kkbaun, rcl_kk_cloud_num_sea, rcl_kk_cloud_num_land;
+  real rcl_const1s, rcl_const7s, rcl_const8s, rdensref, rcl_cdenom1, rcl_cdenom2, rcl_cdenom3;
+  real rcl_const1r, rcl_const2r, rcl_const3r, rcl_const4r, rcl_fac1, rcl_fac2, rcl_const5r, rcl_const6r;
+  real rcl_fzrab;
+  // host-folded (each is exactly the reference's own expression, evaluated once)
+  real zqtmst;        // 1/ptsphy                       cloudsc_c.c:385
+  real zrdcp;         // rd/rcpd                        :387
+  real zrg_r;         // 1/rg                           :390
+  real zrldcp;        // 1/(ralsdcp-ralvdcp)            :391
+  real zinv_tsrg;     // 1/(ptsphy*rg)                  :807
+  real half_rg;       // 0.5*rg                         :1146
+  real zldifdt0;      // rcldiff*ptsphy                 :1088
+  real zldifdt_conv;  // rcldiff_convi*(rcldiff*ptsphy) :1091
+  real zfaci_koop;    // ptsphy/rkooptau                :889
+  real zzco_snow;     // ptsphy*rsnowlin1               :1624
+  real rv_rd;         // rv/rd                          :2011
+  real rg_rpecons;    // rg*rpecons                     :2065
+  real one_m_ramin;   // 1-ramin                        :898
+  int nssopt, ncldtop, laericesed, laericeauto;
+};
+
+// Address-space-4 (constant) pointer: loads through it are scalar (s_load).
+#define CLOUDSC_AS4 __attribute__((address_space(4)))
+template <typename T>
+using cptr = const CLOUDSC_AS4 T*;
+
+// Hide a uniform constant-space pointer from the optimiser.  The ~90 parameters
+// and ~45 field base pointers are all uniform and read with scalar loads; left
+// alone, LLVM hoists every one of them out of the 137-level loop, runs out of
+// SGPRs and spills them into VGPR lanes (v_writelane/v_readlane), or keeps
+// per-field 64-bit VGPR pointers alive (~90 VGPRs).  Laundering the address once
+// per level (or per phase) keeps each scalar load next to its use -- a scalar
+// cache hit -- at no register cost.
+template <typename T>
+__device__ __forceinline__ cptr<T> launder_uniform(cptr<T> p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+template <typename T>
+__device__ __forceinline__ T launder_vgpr(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Real-typed literal: R(0.5) is a double for fp64 and a float for fp32
+// (the JPRB=sp semantics, parkind1.F90:40-43).
+#define R(x) (real)(x)
+
+// FOEALFA (src/common/include/fcttre.func.h; inlined at cloudsc_c.c:588,831,1162-1174)
+template <typename real, typename P>
+__device__ __forceinline__ real foealfa(const P& c, real t) {
+  real x = (fmax(c.rtice, fmin(c.rtwat, t)) - c.rtice) * c.rtwat_rtice_r;
+  return fmin(R(1.0), x * x);            // pow(x,2) == x*x (both rounded once)
+}
+template <typename real, typename P>
+__device__ __forceinline__ real exp_liq(const P& c, real t) { return exp((c.r3les * (t - c.rtt)) / (t - c.r4les)); }
+template <typename real, typename P>
+__device__ __forceinline__ real exp_ice(const P& c, real t) { return exp((c.r3ies * (t - c.rtt)) / (t - c.r4ies)); }
+
+// alfa*R5ALVCP/(T-R4LES)^2 + (1-alfa)*R5ALSCP/(T-R4IES)^2 (cloudsc_c.c:1166,1220)
+template <typename real, typename P>
+__device__ __forceinline__ real foedem_term(const P& c, real t, real alfa) {
+  real dl = t - c.r4les, di = t - c.r4ies;
+  return ((alfa * c.r5alvcp) * (R(1.0) / (dl * dl))) + (((R(1.0) - alfa) * c.r5alscp) * (R(1.0) / (di * di)));
+}
+
+}  // namespace cloudsc

@@ -1,0 +1,602 @@
+// cloudsc_gpu.hip -- libcloudsc_amd.so: the C ABI of include/cloudsc_amd.h on
+// top of the hand-written CDNA4 kernels.
+//
+//   * parameters -> __constant__ mirrors (fp64 + fp32), one copy per device
+//     (replaces the TECLDP device struct + 28 by-value scalars of
+//     src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:383,412-416)
+//   * cloudsc_gpu_run: one launch, NPROMA block -> workgroup, column -> lane
+//   * cloudsc_state_*: device-side expansion from the KLON-column template
+//     (g % klon of the GLOBAL column, so shards are bit-identical to an
+//     unsharded run), per-step timing with HIP events on the state's stream,
+//     and device-side validation statistics against the KLON-column reference.
+//
+// No CPU fallback: every entry point fails with a CLOUDSC_E* code if HIP or
+// the device is unavailable.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "cloudsc_amd.h"
+#include "cloudsc_dev.h"
+#include "cloudsc_kcache.h"
+#include "cloudsc_scc.h"
+
+using namespace cloudsc;
+
+// ---------------------------------------------------------------------------
+// __constant__ parameter mirrors
+// ---------------------------------------------------------------------------
+__constant__ DevParams<double> g_params_dp;
+__constant__ DevParams<float> g_params_sp;
+
+namespace {
+
+thread_local char g_hip_err[256] = "";
+constexpr int kMaxDevices = 64;
+bool g_inited[kMaxDevices] = {false};
+
+int hip_fail(hipError_t e, const char* what) {
+  snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s", what, hipGetErrorString(e));
+  return CLOUDSC_EHIP;
+}
+#define HIPCHK(call)                                  \
+  do {                                                \
+    hipError_t e_ = (call);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #call); \
+  } while (0)
+
+template <typename real>
+DevParams<real> fold_params(const cloudsc_params_t& p) {
+  DevParams<real> d;
+  std::memset(&d, 0, sizeof(d));
+#define CP(n) d.n = (real)p.n
+  CP(ptsphy); CP(rg); CP(rd); CP(retv); CP(rlvtt); CP(rlstt); CP(rtt); CP(rv);
+  CP(r2es); CP(r3les); CP(r3ies); CP(r4les); CP(r4ies); CP(r5les); CP(r5ies); CP(r5alvcp); CP(r5alscp);
+  CP(ralvdcp); CP(ralsdcp); CP(ralfdcp); CP(rtwat); CP(rtice); CP(rtwat_rtice_r); CP(rkoop1); CP(rkoop2);
+  CP(ramid); CP(rprecrhmax); CP(rtaumel); CP(ramin); CP(rlmin); CP(rlcritsnow); CP(rsnowlin2);
+  CP(riceinit); CP(rvice); CP(rvrain); CP(rvsnow); CP(rthomo); CP(rcovpmin); CP(rnice); CP(rcldtopcf);
+  CP(rdepliqrefrate); CP(rdepliqrefdepth); CP(rvrfactor); CP(rclcrit_sea); CP(rclcrit_land);
+  CP(rcl_kkaac); CP(rcl_kkbac); CP(rcl_kkaau); CP(rcl_kkbauq); CP(rcl_kkbaun); CP(rcl_kk_cloud_num_sea);
+  CP(rcl_kk_cloud_num_land); CP(rcl_const1s); CP(rcl_const7s); CP(rcl_const8s); CP(rdensref);
+  CP(rcl_cdenom1); CP(rcl_cdenom2); CP(rcl_cdenom3); CP(rcl_const1r); CP(rcl_const2r); CP(rcl_const3r);
+  CP(rcl_const4r); CP(rcl_fac1); CP(rcl_fac2); CP(rcl_const5r); CP(rcl_const6r); CP(rcl_fzrab);
+#undef CP
+  // Host folding in the working precision: the same single IEEE operation the
+  // reference evaluates per point (x86-64 host float/double arithmetic is IEEE).
+  const real ptsphy = (real)p.ptsphy, rg = (real)p.rg, rd = (real)p.rd, rcpd = (real)p.rcpd;
+  volatile real one = (real)1.0;   // keep the compiler from re-associating
+  d.zqtmst = one / ptsphy;
+  d.zrdcp = rd / rcpd;
+  d.zrg_r = one / rg;
+  d.zrldcp = one / ((real)p.ralsdcp - (real)p.ralvdcp);
+  d.zinv_tsrg = one / (ptsphy * rg);
+  d.half_rg = (real)0.5 * rg;
+  d.zldifdt0 = (real)p.rcldiff * ptsphy;
+  d.zldifdt_conv = (real)p.rcldiff_convi * d.zldifdt0;
+  d.zfaci_koop = ptsphy / (real)p.rkooptau;
+  d.zzco_snow = ptsphy * (real)p.rsnowlin1;
+  d.rv_rd = (real)p.rv / rd;
+  d.rg_rpecons = rg * (real)p.rpecons;
+  d.one_m_ramin = one - (real)p.ramin;
+  d.nssopt = p.nssopt;
+  d.ncldtop = p.ncldtop;
+  d.laericesed = p.laericesed;
+  d.laericeauto = p.laericeauto;
+  return d;
+}
+
+int check_params(const cloudsc_params_t* p) {
+  if (!p) return CLOUDSC_EINVAL;
+  if (p->ncldtop < 2) return CLOUDSC_EINVAL;        // the physics reads level jk-1 (za, ztp1)
+  if (p->nssopt < 0 || p->nssopt > 3) return CLOUDSC_EINVAL;
+  if (!(p->ptsphy > 0.0)) return CLOUDSC_EINVAL;
+  return CLOUDSC_OK;
+}
+
+template <typename real>
+KArgs<real> make_args(const cloudsc_fields_t* f, int ngptot, int nproma, int klev) {
+  KArgs<real> a;
+  a.pt = (const real*)f->pt; a.pq = (const real*)f->pq;
+  a.ttt = (const real*)f->tendency_tmp_t; a.ttq = (const real*)f->tendency_tmp_q;
+  a.tta = (const real*)f->tendency_tmp_a; a.ttcld = (const real*)f->tendency_tmp_cld;
+  a.pvfl = (const real*)f->pvfl; a.pvfi = (const real*)f->pvfi;
+  a.phrsw = (const real*)f->phrsw; a.phrlw = (const real*)f->phrlw; a.pvervel = (const real*)f->pvervel;
+  a.pap = (const real*)f->pap; a.paph = (const real*)f->paph; a.plsm = (const real*)f->plsm;
+  a.ktype = f->ktype;
+  a.plu = (const real*)f->plu; a.psnde = (const real*)f->psnde; a.pmfu = (const real*)f->pmfu;
+  a.pmfd = (const real*)f->pmfd; a.pa = (const real*)f->pa; a.pclv = (const real*)f->pclv;
+  a.psupsat = (const real*)f->psupsat; a.picrit_aer = (const real*)f->picrit_aer;
+  a.pre_ice = (const real*)f->pre_ice; a.pnice = (const real*)f->pnice;
+  a.plude = (real*)f->plude; a.tlt = (real*)f->tendency_loc_t; a.tlq = (real*)f->tendency_loc_q;
+  a.tla = (real*)f->tendency_loc_a; a.tlcld = (real*)f->tendency_loc_cld;
+  a.pcovptot = (real*)f->pcovptot; a.prainfrac = (real*)f->prainfrac_toprfz;
+  a.pfsqlf = (real*)f->pfsqlf; a.pfsqif = (real*)f->pfsqif; a.pfcqnng = (real*)f->pfcqnng;
+  a.pfcqlng = (real*)f->pfcqlng; a.pfsqrf = (real*)f->pfsqrf; a.pfsqsf = (real*)f->pfsqsf;
+  a.pfcqrng = (real*)f->pfcqrng; a.pfcqsng = (real*)f->pfcqsng; a.pfsqltur = (real*)f->pfsqltur;
+  a.pfsqitur = (real*)f->pfsqitur; a.pfplsl = (real*)f->pfplsl; a.pfplsn = (real*)f->pfplsn;
+  a.pfhpsl = (real*)f->pfhpsl; a.pfhpsn = (real*)f->pfhpsn;
+  a.ngptot = ngptot; a.nproma = nproma; a.klev = klev;
+  return a;
+}
+
+bool fields_complete(const cloudsc_fields_t* f) {
+  const void* req[] = {f->pt, f->pq, f->tendency_tmp_t, f->tendency_tmp_q, f->tendency_tmp_a,
+                       f->tendency_tmp_cld, f->pvfl, f->pvfi, f->phrsw, f->phrlw, f->pvervel, f->pap,
+                       f->paph, f->plsm, f->ktype, f->plu, f->psnde, f->pmfu, f->pmfd, f->pa, f->pclv,
+                       f->psupsat, f->plude, f->tendency_loc_t, f->tendency_loc_q, f->tendency_loc_a,
+                       f->tendency_loc_cld, f->pcovptot, f->prainfrac_toprfz, f->pfsqlf, f->pfsqif,
+                       f->pfcqnng, f->pfcqlng, f->pfsqrf, f->pfsqsf, f->pfcqrng, f->pfcqsng,
+                       f->pfsqltur, f->pfsqitur, f->pfplsl, f->pfplsn, f->pfhpsl, f->pfhpsn};
+  for (const void* q : req)
+    if (!q) return false;
+  return true;
+}
+
+// the __constant__ mirror of a precision, as a constant-address-space pointer
+template <typename real> __device__ __forceinline__ cptr<DevParams<real>> dev_params();
+template <> __device__ __forceinline__ cptr<DevParams<double>> dev_params<double>() {
+  return (cptr<DevParams<double>>)&g_params_dp;
+}
+template <> __device__ __forceinline__ cptr<DevParams<float>> dev_params<float>() {
+  return (cptr<DevParams<float>>)&g_params_sp;
+}
+
+}  // namespace
+
+// Kernel entry points.  The KArgs struct is the first explicit kernel argument,
+// i.e. it sits at offset 0 of the kernarg segment; the bodies read it (and the
+// parameter block) through constant-address-space pointers.
+template <typename real>
+__global__ void __launch_bounds__(256) kcache_entry(const KArgs<real> a) {
+  (void)a;
+  cloudsc_kcache_body<real>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), dev_params<real>());
+}
+template <typename real>
+__global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccScratch<real> s) {
+  (void)a;
+  cloudsc_scc_body<real>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), s, dev_params<real>());
+}
+
+// ---------------------------------------------------------------------------
+// plumbing kernels: expansion and validation statistics
+// ---------------------------------------------------------------------------
+// dst[b][L][i] = src[L][(col_offset + b*nproma + i) % klon], L < nlev
+template <typename T, typename S>
+__global__ void expand_kernel(T* __restrict__ dst, const S* __restrict__ src, int nlev, int klon,
+                              int nproma, long long col_offset, long long nblocks) {
+  const long long b = blockIdx.y;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nlev * nproma; e += gridDim.x * blockDim.x) {
+    const int L = e / nproma, i = e - L * nproma;
+    const long long g = col_offset + b * nproma + i;
+    dst[(size_t)b * nlev * nproma + e] = (T)src[(size_t)L * klon + (size_t)(g % klon)];
+  }
+  (void)nblocks;
+}
+
+// One workgroup per NPROMA block: min/max of the field, max|d|, sum|d|, sum|ref|
+// over the active lanes of that block (validate_mod.F90:136-146, with fabs).
+template <typename real>
+__global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld, const double* __restrict__ ref,
+                                                    int nlev, int klon, int nproma, long long ngptot,
+                                                    long long col_offset, double* __restrict__ part) {
+  const long long b = blockIdx.x;
+  const long long bsize = (ngptot - b * nproma) < nproma ? (ngptot - b * nproma) : nproma;
+  double mn = __DBL_MAX__, mx = -__DBL_MAX__, me = 0.0, es = 0.0, rs = 0.0;
+  for (int e = threadIdx.x; e < nlev * nproma; e += blockDim.x) {
+    const int L = e / nproma, i = e - L * nproma;
+    if (i >= bsize) continue;
+    const long long g = col_offset + b * nproma + i;
+    const double v = (double)fld[(size_t)b * nlev * nproma + e];
+    const double r = ref[(size_t)L * klon + (size_t)(g % klon)];
+    const double d = fabs(v - r);
+    mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, d); es += d; rs += fabs(r);
+  }
+  __shared__ double s[5][256];
+  s[0][threadIdx.x] = mn; s[1][threadIdx.x] = mx; s[2][threadIdx.x] = me; s[3][threadIdx.x] = es; s[4][threadIdx.x] = rs;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const int t = threadIdx.x;
+      s[0][t] = fmin(s[0][t], s[0][t + w]); s[1][t] = fmax(s[1][t], s[1][t + w]);
+      s[2][t] = fmax(s[2][t], s[2][t + w]); s[3][t] += s[3][t + w]; s[4][t] += s[4][t + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 5; q++) part[b * 5 + q] = s[q][0];
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+namespace {
+
+int validate_run_args(int device, int precision, int variant, int ngptot, int nproma, int klev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CLOUDSC_ENODEV;
+  if (device < 0 || device >= n || device >= kMaxDevices) return CLOUDSC_ENODEV;
+  if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return CLOUDSC_EINVAL;
+  if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC) return CLOUDSC_EINVAL;
+  if (ngptot <= 0 || nproma <= 0 || nproma > 256 || klev < 2) return CLOUDSC_EINVAL;
+  if (!g_inited[device]) return CLOUDSC_ENOINIT;
+  return CLOUDSC_OK;
+}
+
+template <typename real>
+int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
+           void* scratch) {
+  const KArgs<real> a = make_args<real>(f, ngptot, nproma, klev);
+  const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  if (variant == CLOUDSC_VARIANT_KCACHE) {
+    hipLaunchKernelGGL(kcache_entry<real>, dim3(nblocks), dim3(nproma), 0, st, a);
+  } else {
+    if (!scratch) return CLOUDSC_EINVAL;
+    SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
+    hipLaunchKernelGGL(scc_entry<real>, dim3(nblocks), dim3(nproma), 0, st, a, s);
+  }
+  HIPCHK(hipGetLastError());
+  return CLOUDSC_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI: low level
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int cloudsc_gpu_device_count(int* count) {
+  if (!count) return CLOUDSC_EINVAL;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) { *count = 0; return hip_fail(e, "hipGetDeviceCount"); }
+  *count = n;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_gpu_init(int device, const cloudsc_params_t* params) {
+  int rc = check_params(params);
+  if (rc) return rc;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n || device >= kMaxDevices)
+    return CLOUDSC_ENODEV;
+  HIPCHK(hipSetDevice(device));
+  const DevParams<double> dp = fold_params<double>(*params);
+  const DevParams<float> sp = fold_params<float>(*params);
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_params_dp), &dp, sizeof(dp)));
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_params_sp), &sp, sizeof(sp)));
+  HIPCHK(hipDeviceSynchronize());
+  g_inited[device] = true;
+  return CLOUDSC_OK;
+}
+
+long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev) {
+  if (variant != CLOUDSC_VARIANT_SCC) return 0;
+  if (ngptot <= 0 || nproma <= 0 || klev < 2) return -1;
+  const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  return precision == CLOUDSC_FP64 ? scc_scratch_bytes<double>(nblocks, nproma, klev)
+                                   : scc_scratch_bytes<float>(nblocks, nproma, klev);
+}
+
+int cloudsc_gpu_run(int device, void* stream, int precision, int variant, int ngptot, int nproma,
+                    int klev, const cloudsc_fields_t* f, void* scratch) {
+  int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
+  if (rc) return rc;
+  if (!f || !fields_complete(f)) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(device));
+  hipStream_t st = (hipStream_t)stream;
+  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch)
+                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch);
+}
+
+const char* cloudsc_strerror(int code) {
+  switch (code) {
+    case CLOUDSC_OK: return "success";
+    case CLOUDSC_EINVAL: return "invalid argument";
+    case CLOUDSC_ENODEV: return "no such HIP device";
+    case CLOUDSC_EHIP: return "HIP runtime error";
+    case CLOUDSC_ENOINIT: return "cloudsc_gpu_init not called for this device";
+    case CLOUDSC_ENOMEM: return "out of memory";
+    case CLOUDSC_EIO: return "I/O error";
+    default: return "unknown error";
+  }
+}
+
+const char* cloudsc_last_hip_error(void) { return g_hip_err; }
+
+long long cloudsc_abi_sizeof(int which) {
+  switch (which) {
+    case 0: return sizeof(cloudsc_params_t);
+    case 1: return sizeof(cloudsc_fields_t);
+    case 2: return sizeof(cloudsc_template_t);
+    case 3: return sizeof(cloudsc_reference_t);
+    case 4: return sizeof(cloudsc_stats_t);
+    default: return -1;
+  }
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// C ABI: device-resident dwarf state
+// ---------------------------------------------------------------------------
+struct cloudsc_gpu_state {
+  int device, precision, ngptot, nproma, klev, klon, nblocks;
+  long long col_offset;
+  size_t es;                      // element size
+  hipStream_t stream;
+  hipEvent_t ev0, ev1;
+  cloudsc_fields_t f;             // device pointers
+  void* plude_pristine;
+  void* scratch;
+  size_t scratch_bytes;
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+size_t field_elems(const cloudsc_gpu_state* s, int kind /*0 2d,1 2dh,2 3d,3 1d*/) {
+  const size_t nb = s->nblocks, np = s->nproma, kl = s->klev;
+  switch (kind) {
+    case 0: return nb * kl * np;
+    case 1: return nb * (kl + 1) * np;
+    case 2: return nb * 5 * kl * np;
+    default: return nb * np;
+  }
+}
+// validated field table: pointer slot and shape kind, in cloudsc_field_id order
+void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
+  const cloudsc_fields_t& f = s->f;
+  static const int kinds[CLOUDSC_NVALID] = {0, 0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 2};
+  void* const* slots[CLOUDSC_NVALID] = {
+      &f.plude, &f.pcovptot, &f.prainfrac_toprfz, &f.pfsqlf, &f.pfsqif, &f.pfcqlng, &f.pfcqnng,
+      &f.pfsqrf, &f.pfsqsf, &f.pfcqrng, &f.pfcqsng, &f.pfsqltur, &f.pfsqitur, &f.pfplsl, &f.pfplsn,
+      &f.pfhpsl, &f.pfhpsn, &f.tendency_loc_a, &f.tendency_loc_q, &f.tendency_loc_t, &f.tendency_loc_cld};
+  *kind = kinds[id];
+  return slots[id];
+}
+
+int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
+  s->allocs.push_back(*p);
+  return CLOUDSC_OK;
+}
+
+// upload one template array and expand it into the block-layout device field
+int expand_into(cloudsc_gpu_state* s, void* dst, const void* host_src, int nlev, bool is_int) {
+  const size_t src_bytes = (size_t)nlev * s->klon * (is_int ? sizeof(int) : sizeof(double));
+  void* d_src = nullptr;
+  HIPCHK(hipMalloc(&d_src, src_bytes));
+  hipError_t e = hipMemcpyAsync(d_src, host_src, src_bytes, hipMemcpyHostToDevice, s->stream);
+  if (e == hipSuccess) {
+    const int per = nlev * s->nproma;
+    dim3 grid((per + 255) / 256, s->nblocks);
+    if (is_int)
+      hipLaunchKernelGGL((expand_kernel<int, int>), grid, dim3(256), 0, s->stream, (int*)dst, (const int*)d_src,
+                         nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
+    else if (s->precision == CLOUDSC_FP64)
+      hipLaunchKernelGGL((expand_kernel<double, double>), grid, dim3(256), 0, s->stream, (double*)dst,
+                         (const double*)d_src, nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
+    else
+      hipLaunchKernelGGL((expand_kernel<float, double>), grid, dim3(256), 0, s->stream, (float*)dst,
+                         (const double*)d_src, nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  }
+  hipFree(d_src);
+  if (e != hipSuccess) return hip_fail(e, "expand");
+  return CLOUDSC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, int ngptot, int nproma,
+                         long long col_offset, const cloudsc_template_t* t, const cloudsc_params_t* params) {
+  if (!out || !t || !params || col_offset < 0) return CLOUDSC_EINVAL;
+  *out = nullptr;
+  int rc = cloudsc_gpu_init(device, params);
+  if (rc) return rc;
+  rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KCACHE, ngptot, nproma, t->klev);
+  if (rc) return rc;
+  if (t->klon <= 0) return CLOUDSC_EINVAL;
+  const void* req[] = {t->pt, t->pq, t->tendency_tmp_t, t->tendency_tmp_q, t->tendency_tmp_a,
+                       t->tendency_tmp_cld, t->pvfl, t->pvfi, t->phrsw, t->phrlw, t->pvervel, t->pap,
+                       t->paph, t->plsm, t->ktype, t->plu, t->plude, t->psnde, t->pmfu, t->pmfd, t->pa,
+                       t->pclv, t->psupsat};
+  for (const void* q : req)
+    if (!q) return CLOUDSC_EINVAL;
+  if (params->laericesed && !t->pre_ice) return CLOUDSC_EINVAL;
+  if (params->laericeauto && (!t->picrit_aer || !t->pnice)) return CLOUDSC_EINVAL;
+
+  cloudsc_gpu_state* s = new cloudsc_gpu_state();
+  s->device = device; s->precision = precision; s->ngptot = ngptot; s->nproma = nproma;
+  s->klev = t->klev; s->klon = t->klon; s->col_offset = col_offset;
+  s->nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  s->es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
+  std::memset(&s->f, 0, sizeof(s->f));
+  auto fail = [&](int r) { cloudsc_state_destroy(s); return r; };
+  if (hipSetDevice(device) != hipSuccess) return fail(CLOUDSC_ENODEV);
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
+  if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) return fail(CLOUDSC_EHIP);
+
+  const size_t n2 = field_elems(s, 0) * s->es, n2h = field_elems(s, 1) * s->es;
+  const size_t n3 = field_elems(s, 2) * s->es, n1 = field_elems(s, 3) * s->es;
+  const int kl = s->klev;
+  struct In { const void** dst; const void* src; int nlev; size_t bytes; bool is_int; };
+  cloudsc_fields_t& f = s->f;
+  void* plude_dev = nullptr;
+  In ins[] = {
+      {&f.pt, t->pt, kl, n2, false}, {&f.pq, t->pq, kl, n2, false},
+      {&f.tendency_tmp_t, t->tendency_tmp_t, kl, n2, false}, {&f.tendency_tmp_q, t->tendency_tmp_q, kl, n2, false},
+      {&f.tendency_tmp_a, t->tendency_tmp_a, kl, n2, false}, {&f.tendency_tmp_cld, t->tendency_tmp_cld, 5 * kl, n3, false},
+      {&f.pvfl, t->pvfl, kl, n2, false}, {&f.pvfi, t->pvfi, kl, n2, false}, {&f.phrsw, t->phrsw, kl, n2, false},
+      {&f.phrlw, t->phrlw, kl, n2, false}, {&f.pvervel, t->pvervel, kl, n2, false}, {&f.pap, t->pap, kl, n2, false},
+      {&f.paph, t->paph, kl + 1, n2h, false}, {&f.plsm, t->plsm, 1, n1, false},
+      {(const void**)&f.ktype, t->ktype, 1, (size_t)s->nblocks * nproma * sizeof(int), true},
+      {&f.plu, t->plu, kl, n2, false}, {&f.psnde, t->psnde, kl, n2, false}, {&f.pmfu, t->pmfu, kl, n2, false},
+      {&f.pmfd, t->pmfd, kl, n2, false}, {&f.pa, t->pa, kl, n2, false}, {&f.pclv, t->pclv, 5 * kl, n3, false},
+      {&f.psupsat, t->psupsat, kl, n2, false},
+      {&f.plcrit_aer, t->plcrit_aer, kl, n2, false}, {&f.picrit_aer, t->picrit_aer, kl, n2, false},
+      {&f.pre_ice, t->pre_ice, kl, n2, false}, {&f.pccn, t->pccn, kl, n2, false}, {&f.pnice, t->pnice, kl, n2, false},
+      {(const void**)&plude_dev, t->plude, kl, n2, false},
+  };
+  for (In& in : ins) {
+    if (!in.src) continue;
+    void* p = nullptr;
+    if ((rc = dalloc(s, &p, in.bytes))) return fail(rc);
+    if ((rc = expand_into(s, p, in.src, in.nlev, in.is_int))) return fail(rc);
+    *in.dst = p;
+  }
+  s->plude_pristine = plude_dev;
+  struct Out { void** dst; size_t bytes; };
+  Out outs[] = {{&f.plude, n2}, {&f.tendency_loc_t, n2}, {&f.tendency_loc_q, n2}, {&f.tendency_loc_a, n2},
+                {&f.tendency_loc_cld, n3}, {&f.pcovptot, n2}, {&f.prainfrac_toprfz, n1},
+                {&f.pfsqlf, n2h}, {&f.pfsqif, n2h}, {&f.pfcqnng, n2h}, {&f.pfcqlng, n2h}, {&f.pfsqrf, n2h},
+                {&f.pfsqsf, n2h}, {&f.pfcqrng, n2h}, {&f.pfcqsng, n2h}, {&f.pfsqltur, n2h}, {&f.pfsqitur, n2h},
+                {&f.pfplsl, n2h}, {&f.pfplsn, n2h}, {&f.pfhpsl, n2h}, {&f.pfhpsn, n2h}};
+  for (Out& o : outs) {
+    if ((rc = dalloc(s, o.dst, o.bytes))) return fail(rc);
+    if (hipMemsetAsync(*o.dst, 0xff, o.bytes, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);  // NaN
+  }
+  if (hipMemcpyAsync(f.plude, s->plude_pristine, n2, hipMemcpyDeviceToDevice, s->stream) != hipSuccess)
+    return fail(CLOUDSC_EHIP);
+  if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);
+  *out = s;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_fields(const cloudsc_gpu_state_t* s, cloudsc_fields_t* out) {
+  if (!s || !out) return CLOUDSC_EINVAL;
+  *out = s->f;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_reset(cloudsc_gpu_state_t* s) {
+  if (!s) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipMemcpyAsync(s->f.plude, s->plude_pristine, field_elems(s, 0) * s->es, hipMemcpyDeviceToDevice,
+                        s->stream));
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) {
+  if (!s || reps <= 0) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  if (variant == CLOUDSC_VARIANT_SCC && !s->scratch) {     // SCC temporaries, allocated on first use
+    s->scratch_bytes = (size_t)cloudsc_gpu_scratch_bytes(s->precision, variant, s->ngptot, s->nproma, s->klev);
+    int rc0 = dalloc(s, &s->scratch, s->scratch_bytes);
+    if (rc0) return rc0;
+  }
+  std::vector<hipEvent_t> ev(2 * (size_t)reps);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  int rc = CLOUDSC_OK;
+  for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
+    rc = cloudsc_state_reset(s);                                   // outside the event pair
+    if (rc) break;
+    HIPCHK(hipEventRecord(ev[2 * r], s->stream));
+    rc = cloudsc_gpu_run(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f,
+                         s->scratch);
+    HIPCHK(hipEventRecord(ev[2 * r + 1], s->stream));
+  }
+  hipError_t e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess && rc == CLOUDSC_OK) rc = hip_fail(e, "hipStreamSynchronize");
+  for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
+    float t = 0.f;
+    e = hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]);
+    if (e != hipSuccess) rc = hip_fail(e, "hipEventElapsedTime");
+    if (ms) ms[r] = t;
+  }
+  for (auto& x : ev) hipEventDestroy(x);
+  return rc;
+}
+
+int cloudsc_state_sync(cloudsc_gpu_state_t* s) {
+  if (!s) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return CLOUDSC_OK;
+}
+
+long long cloudsc_state_field_elems(const cloudsc_gpu_state_t* s, int id) {
+  if (!s || id < 0 || id >= CLOUDSC_NVALID) return -1;
+  int kind;
+  valid_slot(s, id, &kind);
+  return (long long)field_elems(s, kind);
+}
+
+int cloudsc_state_download(cloudsc_gpu_state_t* s, int id, double* host) {
+  if (!s || !host || id < 0 || id >= CLOUDSC_NVALID) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  int kind;
+  void* const* slot = valid_slot(s, id, &kind);
+  const size_t n = field_elems(s, kind);
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (s->precision == CLOUDSC_FP64) {
+    HIPCHK(hipMemcpy(host, *slot, n * sizeof(double), hipMemcpyDeviceToHost));
+  } else {
+    std::vector<float> tmp(n);
+    HIPCHK(hipMemcpy(tmp.data(), *slot, n * sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; i++) host[i] = tmp[i];
+  }
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* ref, cloudsc_stats_t* stats) {
+  if (!s || !ref || !stats || ref->klon <= 0 || ref->klev != s->klev) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  double* part = nullptr;
+  double* dref = nullptr;
+  HIPCHK(hipMalloc(&part, (size_t)s->nblocks * 5 * sizeof(double)));
+  const size_t max_ref = (size_t)5 * (s->klev + 1) * ref->klon;
+  hipError_t e = hipMalloc(&dref, max_ref * sizeof(double));
+  std::vector<double> h((size_t)s->nblocks * 5);
+  for (int id = 0; id < CLOUDSC_NVALID && e == hipSuccess; id++) {
+    int kind;
+    void* const* slot = valid_slot(s, id, &kind);
+    const int nlev = kind == 0 ? s->klev : kind == 1 ? s->klev + 1 : kind == 2 ? 5 * s->klev : 1;
+    if (!ref->field[id]) { e = hipErrorInvalidValue; break; }
+    e = hipMemcpy(dref, ref->field[id], (size_t)nlev * ref->klon * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) break;
+    if (s->precision == CLOUDSC_FP64)
+      hipLaunchKernelGGL(stats_kernel<double>, dim3(s->nblocks), dim3(256), 0, s->stream, (const double*)*slot,
+                         dref, nlev, ref->klon, s->nproma, (long long)s->ngptot, s->col_offset, part);
+    else
+      hipLaunchKernelGGL(stats_kernel<float>, dim3(s->nblocks), dim3(256), 0, s->stream, (const float*)*slot,
+                         dref, nlev, ref->klon, s->nproma, (long long)s->ngptot, s->col_offset, part);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) break;
+    cloudsc_stats_t t = {__DBL_MAX__, -__DBL_MAX__, 0.0, 0.0, 0.0};
+    for (int b = 0; b < s->nblocks; b++) {            // block order: deterministic
+      t.minval = fmin(t.minval, h[b * 5 + 0]); t.maxval = fmax(t.maxval, h[b * 5 + 1]);
+      t.maxerr = fmax(t.maxerr, h[b * 5 + 2]); t.errsum += h[b * 5 + 3]; t.refsum += h[b * 5 + 4];
+    }
+    stats[id] = t;
+  }
+  hipFree(part);
+  hipFree(dref);
+  if (e != hipSuccess) return hip_fail(e, "validate");
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_destroy(cloudsc_gpu_state_t* s) {
+  if (!s) return CLOUDSC_OK;
+  hipSetDevice(s->device);
+  if (s->stream) hipStreamSynchronize(s->stream);
+  for (void* p : s->allocs) hipFree(p);
+  if (s->ev0) hipEventDestroy(s->ev0);
+  if (s->ev1) hipEventDestroy(s->ev1);
+  if (s->stream) hipStreamDestroy(s->stream);
+  delete s;
+  return CLOUDSC_OK;
+}
+
+}  // extern "C"

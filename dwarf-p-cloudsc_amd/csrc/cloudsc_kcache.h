@@ -1,0 +1,946 @@
+// cloudsc_kcache.h -- the CLOUDSC column physics for CDNA4 (gfx950), split into
+// per-level phases, and the SCC-k-caching kernel body built from them.
+//
+// Semantics: the reference kernel src/cloudsc_c/cloudsc/cloudsc_c.c:19-2587
+// (restated, bit-exact on the CPU, by oracle/cloudsc_oracle.c).  Structure:
+// the k-caching layout of src/cloudsc_gpu/cloudsc_gpu_scc_k_caching_mod.F90 --
+// an NPROMA block is one workgroup, a column is one lane, and ONE fused loop
+// walks the levels top-down.  Everything the reference keeps in level-sized
+// temporaries (ztp1, za, zqx, zqx0, zlneg, zqxn2d, zfoealfa, zpfplsx, ...) is
+// consumed at the level that produces it, so the only state that survives an
+// iteration is a handful of registers (CarryState): T/A/PAP of the level above,
+// zanewm1, zqxnm1[ql,qi], zpfplsx[qi,qr,qs], zcovptot, zcovpmax, zcldtopdist,
+// prainfrac, and the six running flux sums of section 8 (which the CUDA
+// k-caching kernel re-reads from HBM every level, cloudsc_c_k_caching.cu:2557-2576;
+// here they never leave the register file).  HBM traffic is the compulsory
+// one: each input element read once, each output element written once
+// (56,036 B/column in fp64).
+//
+// Latency hiding: only NGPTOT/64 waves exist (2560 at 163840 columns, 2.5 per
+// SIMD), so the loop software-pipelines its loads: the inputs of level k+1 are
+// issued before the physics of level k runs (LevelIn `nxt`), and the fields the
+// physics needs one level ahead (paph, pmfu, pmfd, plu) two levels ahead.
+//
+// Arithmetic keeps the reference's operand order (hipcc -ffp-contract=off, so
+// no FMA contraction); the only expected differences vs the CPU are the
+// last-ulp results of OCML exp/pow vs glibc.
+#pragma once
+#include "cloudsc_dev.h"
+
+namespace cloudsc {
+
+template <typename real>
+struct KArgs {
+  const real *pt, *pq, *ttt, *ttq, *tta, *ttcld, *pvfl, *pvfi, *phrsw, *phrlw, *pvervel;
+  const real *pap, *paph, *plsm;
+  const int *ktype;
+  const real *plu, *psnde, *pmfu, *pmfd, *pa, *pclv, *psupsat, *picrit_aer, *pre_ice, *pnice;
+  real *plude, *tlt, *tlq, *tla, *tlcld, *pcovptot, *prainfrac;
+  real *pfsqlf, *pfsqif, *pfcqnng, *pfcqlng, *pfsqrf, *pfsqsf, *pfcqrng, *pfcqsng;
+  real *pfsqltur, *pfsqitur, *pfplsl, *pfplsn, *pfhpsl, *pfhpsn;
+  int ngptot, nproma, klev;
+};
+
+enum { QL = 0, QI = 1, QR = 2, QS = 3, QV = 4 };
+
+// Field access = uniform element index (SGPR arithmetic on a uniform base
+// pointer) + the lane's byte offset (one shared 32-bit VGPR).  This is the
+// global_load/store "saddr" form: no per-field 64-bit VGPR pointers.
+template <typename T>
+__device__ __forceinline__ T ldg(const T* ubase, size_t uidx, unsigned lane_bytes) {
+  return *(const T*)((const char*)(ubase + uidx) + lane_bytes);
+}
+template <typename T>
+__device__ __forceinline__ void stg(T* ubase, size_t uidx, unsigned lane_bytes, T v) {
+  *(T*)((char*)(ubase + uidx) + lane_bytes) = v;
+}
+
+// Per-level inputs of one column (the prefetch unit).
+template <typename real>
+struct LevelIn {
+  real pt, pq, ttt, ttq, tta, pa, pap, phrsw, phrlw, pvervel, plude, psnde, psupsat, pvfl, pvfi;
+  real pclv[4], ttcld[4];
+  real pre_ice, picrit_aer, pnice;      // aerosol inputs, loaded only under LAERICESED/LAERICEAUTO
+};
+
+// Values of the neighbouring levels the physics of level k reads.
+template <typename real>
+struct Neighbors {
+  real paph_k, paph_n;                  // paph(k), paph(k+1)
+  real pmfu_k, pmfd_k, pmfu_n, pmfd_n;  // mass fluxes at k and k+1
+  real plu_n;                           // plu(k+1)
+};
+
+// Column constants.
+template <typename real>
+struct ColConst {
+  real paph_sfc, kk_const, kk_lcrit, kk_pow;
+  int ktype;
+};
+
+// State carried from level k to level k+1.
+template <typename real>
+struct CarryState {
+  real t_prev, a_prev, pap_prev, zanewm1, zcovptot, zcovpmax, zcldtopdist, rainfrac;
+  real qxnm1_l, qxnm1_i;                // zqxnm1 of the non-falling condensates
+  real pfx_i, pfx_r, pfx_s;             // zpfplsx[qi,qr,qs] arriving at level k
+  real fl_lf, fl_if, fl_lng, fl_nng, fl_ltur, fl_itur;  // running flux sums (section 8)
+};
+
+// Result of section 1 at one level (the reference's level-sized temporaries).
+template <typename real>
+struct LevelState {
+  real ztp1, za, zaorig, zfoealfa, ttend, qtend;
+  real zqx[5], zqx0[5], zlneg[4];
+};
+
+// Result of the physics at one level.
+template <typename real>
+struct PhysOut {
+  real zqxn[4];                         // zqxn2d(k), zero above NCLDTOP
+  real plude_k, atend, ctend[4], zcovptot_out;
+};
+
+template <typename real>
+__device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& A, const DevParams<real>& c,
+                                           size_t u2, size_t u3, int k, int klev, int nproma, unsigned lo,
+                                           bool physics) {
+  const size_t i = u2 + (size_t)k * nproma;
+  L.pt = ldg(A.pt, i, lo); L.pq = ldg(A.pq, i, lo); L.ttt = ldg(A.ttt, i, lo); L.ttq = ldg(A.ttq, i, lo);
+  L.tta = ldg(A.tta, i, lo); L.pa = ldg(A.pa, i, lo); L.pap = ldg(A.pap, i, lo);
+  L.plude = ldg((const real*)A.plude, i, lo); L.pvfl = ldg(A.pvfl, i, lo); L.pvfi = ldg(A.pvfi, i, lo);
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const size_t j = u3 + ((size_t)m * klev + k) * nproma;
+    L.pclv[m] = ldg(A.pclv, j, lo);
+    L.ttcld[m] = ldg(A.ttcld, j, lo);
+  }
+  if (physics) {
+    L.phrsw = ldg(A.phrsw, i, lo); L.phrlw = ldg(A.phrlw, i, lo); L.pvervel = ldg(A.pvervel, i, lo);
+    L.psnde = ldg(A.psnde, i, lo); L.psupsat = ldg(A.psupsat, i, lo);
+    L.pre_ice = c.laericesed ? ldg(A.pre_ice, i, lo) : R(0.0);
+    L.picrit_aer = c.laericeauto ? ldg(A.picrit_aer, i, lo) : R(0.0);
+    L.pnice = c.laericeauto ? ldg(A.pnice, i, lo) : R(0.0);
+  }
+}
+
+// ===== 1. initial values, tidy-up, FOEALFA at one level (cloudsc_c.c:462-575, 588, 625) =====
+template <typename real>
+__device__ __forceinline__ void init_level(const DevParams<real>& c, const LevelIn<real>& in, LevelState<real>& s) {
+  s.ztp1 = in.pt + c.ptsphy * in.ttt;
+  real* zqx = s.zqx;
+  real* zlneg = s.zlneg;
+  zqx[QV] = in.pq + c.ptsphy * in.ttq;
+  s.zqx0[QV] = zqx[QV];
+  real za = in.pa + c.ptsphy * in.tta;
+  s.zaorig = za;
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    zqx[m] = in.pclv[m] + c.ptsphy * in.ttcld[m];
+    s.zqx0[m] = zqx[m];
+    zlneg[m] = R(0.0);
+  }
+  real ttend = R(0.0), qtend = R(0.0);
+  // tidy up very small cloud cover or total cloud water (:519-541)
+  if (zqx[QL] + zqx[QI] < c.rlmin || za < c.ramin) {
+    real zqadj;
+    zlneg[QL] = zlneg[QL] + zqx[QL];
+    zqadj = zqx[QL] * c.zqtmst;
+    qtend = qtend + zqadj;
+    ttend = ttend - c.ralvdcp * zqadj;
+    zqx[QV] = zqx[QV] + zqx[QL];
+    zqx[QL] = R(0.0);
+    zlneg[QI] = zlneg[QI] + zqx[QI];
+    zqadj = zqx[QI] * c.zqtmst;
+    qtend = qtend + zqadj;
+    ttend = ttend - c.ralsdcp * zqadj;
+    zqx[QV] = zqx[QV] + zqx[QI];
+    zqx[QI] = R(0.0);
+    za = R(0.0);
+  }
+  // tidy up small CLV variables (:547-575)
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    if (zqx[m] < c.rlmin) {
+      zlneg[m] = zlneg[m] + zqx[m];
+      const real zqadj = zqx[m] * c.zqtmst;
+      qtend = qtend + zqadj;
+      if (m == QL || m == QR) ttend = ttend - c.ralvdcp * zqadj;   // iphase 1
+      else ttend = ttend - c.ralsdcp * zqadj;                        // iphase 2
+      zqx[QV] = zqx[QV] + zqx[m];
+      zqx[m] = R(0.0);
+    }
+  }
+  s.zfoealfa = foealfa<real>(c, s.ztp1);
+  s.za = fmax(R(0.0), fmin(R(1.0), za));    // clip cloud fraction (:625)
+  s.ttend = ttend;
+  s.qtend = qtend;
+}
+
+// ===== 3.-6. physics of one level ncldtop <= k (cloudsc_c.c:732-2508) =====
+template <typename real>
+__device__ __forceinline__ void physics_level(const DevParams<real>& c, const int k, const int klev,
+                                              const int ncldtop0, const LevelIn<real>& in,
+                                              const Neighbors<real>& nb, const ColConst<real>& cc,
+                                              LevelState<real>& ls, CarryState<real>& cs, PhysOut<real>& po) {
+  const real zepsilon = R(100.0) * (sizeof(real) == 8 ? (real)__DBL_EPSILON__ : (real)__FLT_EPSILON__);
+  const real zepsec = R(1.0e-14);
+  const real ztw1 = R(1329.31000000000), ztw2 = R(0.00746150000000000), ztw3 = R(85000.0000000000);
+  const real ztw4 = R(40.6370000000000), ztw5 = R(275.000000000000);
+  const real ztp1 = ls.ztp1, za = ls.za, zaorig = ls.zaorig, zfoealfa = ls.zfoealfa;
+  const real* zqx = ls.zqx;
+  const real* zqx0 = ls.zqx0;
+  real& ttend = ls.ttend;
+  real& qtend = ls.qtend;
+  real* zqxn = po.zqxn;
+  real* ctend = po.ctend;
+  real& plude_k = po.plude_k;
+  real& atend = po.atend;
+    const real pap_k = in.pap;
+    // saturation values (:583-609)
+    const real e_liq = exp_liq<real>(c, ztp1), e_ice = exp_ice<real>(c, ztp1);
+    const real zfoeewmt = fmin((c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)) / pap_k, R(0.5));
+    const real zqsmix = zfoeewmt / (R(1.0) - c.retv * zfoeewmt);
+    const real zalfa_d = fmax(R(0.0), copysign(R(1.0), ztp1 - c.rtt));
+    real zfoeew = fmin((zalfa_d * (c.r2es * e_liq) + (R(1.0) - zalfa_d) * (c.r2es * e_ice)) / pap_k, R(0.5));
+    zfoeew = fmin(R(0.5), zfoeew);
+    const real zqsice = zfoeew / (R(1.0) - c.retv * zfoeew);
+    const real zfoeeliqt = fmin((c.r2es * e_liq) / pap_k, R(0.5));
+    const real zqsliq = zfoeeliqt / (R(1.0) - c.retv * zfoeeliqt);
+    // liquid/ice fractions (:628-636)
+    const real zli = zqx[QL] + zqx[QI];
+    real zliqfrac = R(0.0), zicefrac = R(0.0);
+    if (zli > c.rlmin) {
+      zliqfrac = zqx[QL] / zli;
+      zicefrac = R(1.0) - zliqfrac;
+    }
+
+    // ===== 3. physics (:732-2508) =====
+    real zqxfg[5];
+  #pragma unroll
+    for (int m = 0; m < 5; m++) zqxfg[m] = zqx[m];
+    // zsolqa is dense in the reference; the entries that can become non-zero
+    // are kept as named scalars sa_<a><b> == zsolqa[a][b] (C indexing).
+    real sa_ll = 0, sa_lv = 0, sa_vl = 0, sa_ii = 0, sa_iv = 0, sa_vi = 0, sa_ss = 0;
+    real sa_li = 0, sa_il = 0, sa_ls = 0, sa_sl = 0, sa_lr = 0, sa_rl = 0, sa_rr = 0;
+    real sa_ir = 0, sa_ri = 0, sa_sr = 0, sa_rs = 0, sa_rv = 0, sa_vr = 0, sa_sv = 0, sa_vs = 0;
+    // zsolqb non-zeros: [ql][ql], [qi][qi] (subsidence), [qi][qs] (snow autoconv), [ql][qs] (riming)
+    real sb_ll = 0, sb_ii = 0, sb_is = 0, sb_ls = 0;
+    real conv_src_l = 0, conv_src_i = 0, conv_sink = 0, psup_l = 0, psup_i = 0;
+    real fsrc_i = 0, fsrc_r = 0, fsrc_s = 0;
+    real zqpretot = R(0.0), zsolab = R(0.0), zsolac = R(0.0);
+
+    // 3.0 derived variables (:799-841)
+    const real zdp = nb.paph_n - nb.paph_k;
+    const real zgdp = c.rg / zdp;
+    const real zrho = pap_k / (c.rd * ztp1);
+    const real zdtgdp = c.ptsphy * zgdp;
+    const real zrdtgdp = zdp * c.zinv_tsrg;
+    real zfacw, zfaci, zfac, zcor;
+    { const real d = ztp1 - c.r4les; zfacw = c.r5les / (d * d); }
+    { const real d = ztp1 - c.r4ies; zfaci = c.r5ies / (d * d); }
+    zcor = R(1.0) / (R(1.0) - c.retv * zfoeew);
+    const real zdqsicedt = (zfaci * zcor) * zqsice;
+    const real zcorqsice = R(1.0) + c.ralsdcp * zdqsicedt;
+    zfac = zfoealfa * zfacw + (R(1.0) - zfoealfa) * zfaci;
+    zcor = R(1.0) / (R(1.0) - c.retv * zfoeewmt);
+    const real zdqsmixdt = (zfac * zcor) * zqsmix;
+    const real zcorqsmix = R(1.0) + (zfoealfa * c.ralvdcp + (R(1.0) - zfoealfa) * c.ralsdcp) * zdqsmixdt;
+    const real zevaplimmix = fmax((zqsmix - zqx[QV]) / zcorqsmix, R(0.0));
+    real ztmpa = R(1.0) / fmax(za, zepsec);
+    real zliqcld = zqx[QL] * ztmpa;
+    real zicecld = zqx[QI] * ztmpa;
+    real zlicld = zliqcld + zicecld;
+
+    // evaporate very small amounts of liquid and ice (:846-859)
+    if (zqx[QL] < c.rlmin) { sa_lv = zqx[QL]; sa_vl = -zqx[QL]; }
+    if (zqx[QI] < c.rlmin) { sa_iv = zqx[QI]; sa_vi = -zqx[QI]; }
+
+    // 3.1 ice supersaturation adjustment (:874-954)
+    const real zfokoop = fmin(c.rkoop1 - c.rkoop2 * ztp1, (c.r2es * e_liq) * R(1.0) / (c.r2es * e_ice));
+    if (c.nssopt == 0 || ztp1 >= c.rtt) {
+      zfac = R(1.0);
+      zfaci = R(1.0);
+    } else {
+      zfac = za + zfokoop * (R(1.0) - za);
+      zfaci = c.zfaci_koop;
+    }
+    real zsupsat;
+    if (za > c.one_m_ramin) {
+      zsupsat = fmax((zqx[QV] - zfac * zqsice) / zcorqsice, R(0.0));
+    } else {
+      const real zqp1env = (zqx[QV] - za * zqsice) / fmax(R(1.0) - za, zepsilon);
+      zsupsat = fmax(((R(1.0) - za) * (zqp1env - zfac * zqsice)) / zcorqsice, R(0.0));
+    }
+    const bool warm_homo = ztp1 > c.rthomo;
+    if (zsupsat > zepsec) {
+      if (warm_homo) {
+        sa_vl = sa_vl + zsupsat; sa_lv = sa_lv - zsupsat; zqxfg[QL] = zqxfg[QL] + zsupsat;
+      } else {
+        sa_vi = sa_vi + zsupsat; sa_iv = sa_iv - zsupsat; zqxfg[QI] = zqxfg[QI] + zsupsat;
+      }
+      zsolac = (R(1.0) - za) * zfaci;
+    }
+    if (in.psupsat > zepsec) {
+      if (warm_homo) {
+        sa_ll = sa_ll + in.psupsat; psup_l = in.psupsat; zqxfg[QL] = zqxfg[QL] + in.psupsat;
+      } else {
+        sa_ii = sa_ii + in.psupsat; psup_i = in.psupsat; zqxfg[QI] = zqxfg[QI] + in.psupsat;
+      }
+      zsolac = (R(1.0) - za) * zfaci;
+    }
+
+    // 3.2 detrainment from convection (:967-987)
+    if (k < klev - 1) {
+      plude_k = plude_k * zdtgdp;
+      if (nb.plu_n > zepsec && plude_k > c.rlmin) {
+        zsolac = zsolac + plude_k / nb.plu_n;
+        conv_src_l = zfoealfa * plude_k;
+        conv_src_i = (R(1.0) - zfoealfa) * plude_k;
+        sa_ll = sa_ll + conv_src_l;
+        sa_ii = sa_ii + conv_src_i;
+      } else {
+        plude_k = R(0.0);
+      }
+      sa_ss = sa_ss + in.psnde * zdtgdp;
+    }
+
+    // 3.3 subsidence source from the layer above + evaporation (:1002-1058)
+    if (k > ncldtop0) {
+      const real zmf = fmax(R(0.0), (nb.pmfu_k + nb.pmfd_k) * zdtgdp);
+      real zacust = zmf * cs.zanewm1;
+      const real zlcust_l = zmf * cs.qxnm1_l;
+      const real zlcust_i = zmf * cs.qxnm1_i;
+      conv_src_l = conv_src_l + zlcust_l;
+      conv_src_i = conv_src_i + zlcust_i;
+      const real zdtdp = ((c.zrdcp * R(0.5)) * (cs.t_prev + ztp1)) / nb.paph_k;
+      const real zdtforc = zdtdp * (pap_k - cs.pap_prev);
+      const real zdqs = (cs.zanewm1 * zdtforc) * zdqsmixdt;
+      real zlfinalsum = R(0.0);
+      {
+        real zlfinal = fmax(R(0.0), zlcust_l - zdqs);
+        const real zevap = fmin(zlcust_l - zlfinal, zevaplimmix);
+        zlfinal = zlcust_l - zevap;
+        zlfinalsum = zlfinalsum + zlfinal;
+        sa_ll = sa_ll + zlcust_l; sa_lv = sa_lv + zevap; sa_vl = sa_vl - zevap;
+      }
+      {
+        real zlfinal = fmax(R(0.0), zlcust_i - zdqs);
+        const real zevap = fmin(zlcust_i - zlfinal, zevaplimmix);
+        zlfinal = zlcust_i - zevap;
+        zlfinalsum = zlfinalsum + zlfinal;
+        sa_ii = sa_ii + zlcust_i; sa_iv = sa_iv + zevap; sa_vi = sa_vi - zevap;
+      }
+      if (zlfinalsum < zepsec) zacust = R(0.0);
+      zsolac = zsolac + zacust;
+    }
+
+    // subsidence sink of cloud to the layer below (:1064-1075)
+    if (k < klev - 1) {
+      const real zmfdn = fmax(R(0.0), (nb.pmfu_n + nb.pmfd_n) * zdtgdp);
+      zsolab = zsolab + zmfdn;
+      sb_ll = sb_ll + zmfdn;
+      sb_ii = sb_ii + zmfdn;
+      conv_sink = zmfdn;
+    }
+
+    // 3.4 erosion of clouds by turbulent mixing (:1087-1118)
+    const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? c.zldifdt_conv : c.zldifdt0;
+    if (zli > zepsec) {
+      const real ze = zldifdt * fmax(zqsmix - zqx[QV], R(0.0));
+      real zleros = za * ze;
+      zleros = fmin(zleros, zevaplimmix);
+      zleros = fmin(zleros, zli);
+      const real zaeros = zleros / zlicld;
+      zsolac = zsolac - zaeros;
+      sa_lv = sa_lv + zliqfrac * zleros; sa_vl = sa_vl - zliqfrac * zleros;
+      sa_iv = sa_iv + zicefrac * zleros; sa_vi = sa_vi - zicefrac * zleros;
+    }
+
+    // 3.4 condensation/evaporation due to dqsat/dt: two Newton steps (:1137-1182)
+    real zdqs;
+    {
+      const real zdtdp = (c.zrdcp * ztp1) / pap_k;
+      const real zdpmxdt = zdp * c.zqtmst;
+      const real zmfdn = (k < klev - 1) ? nb.pmfu_n + nb.pmfd_n : R(0.0);
+      real zwtot = in.pvervel + c.half_rg * (nb.pmfu_k + nb.pmfd_k + zmfdn);
+      zwtot = fmin(zdpmxdt, fmax(-zdpmxdt, zwtot));
+      const real zzzdt = in.phrsw + in.phrlw;
+      const real zdtdiab = fmin(zdpmxdt * zdtdp, fmax(-zdpmxdt * zdtdp, zzzdt)) * c.ptsphy + c.ralfdcp * R(0.0);
+      const real zdtforc = (zdtdp * zwtot) * c.ptsphy + zdtdiab;
+      real tt = fmax(ztp1 + zdtforc, R(160.0));
+      real qsm = zqsmix;
+      const real zqp = R(1.0) / pap_k;
+  #pragma unroll
+      for (int it = 0; it < 2; it++) {
+        const real a = foealfa<real>(c, tt);
+        real zqsat = (c.r2es * (a * exp_liq<real>(c, tt) + (R(1.0) - a) * exp_ice<real>(c, tt))) * zqp;
+        zqsat = fmin(R(0.5), zqsat);
+        const real zcor2 = R(1.0) / (R(1.0) - c.retv * zqsat);
+        zqsat = zqsat * zcor2;
+        const real zcond = (qsm - zqsat) / (R(1.0) + (zqsat * zcor2) * foedem_term<real>(c, tt, a));
+        tt = tt + (a * c.ralvdcp + (R(1.0) - a) * c.ralsdcp) * zcond;
+        qsm = qsm - zcond;
+      }
+      zdqs = qsm - zqsmix;
+    }
+
+    // 3.4a evaporation of clouds (:1189-1207)
+    if (zdqs > R(0.0)) {
+      real zlevap = za * fmin(zdqs, zlicld);
+      zlevap = fmin(zlevap, zevaplimmix);
+      zlevap = fmin(zlevap, fmax(zqsmix - zqx[QV], R(0.0)));
+      sa_lv = sa_lv + zliqfrac * zlevap; sa_vl = sa_vl - zliqfrac * zlevap;
+      sa_iv = sa_iv + zicefrac * zlevap; sa_vi = sa_vi - zicefrac * zlevap;
+    }
+    // 3.4b(1) increase of cloud water in existing clouds (:1213-1250)
+    if (zdqs <= -c.rlmin && za > zepsec) {
+      real zlcond1 = fmax(-zdqs, R(0.0));
+      real zcdmax;
+      if (za > R(0.99)) {
+        const real zcor3 = R(1.0) / (R(1.0) - c.retv * zqsmix);
+        zcdmax = (zqx[QV] - zqsmix) / (R(1.0) + (zcor3 * zqsmix) * foedem_term<real>(c, ztp1, zfoealfa));
+      } else {
+        zcdmax = (zqx[QV] - za * zqsmix) / za;
+      }
+      zlcond1 = fmax(fmin(zlcond1, zcdmax), R(0.0));
+      zlcond1 = za * zlcond1;
+      if (zlcond1 < c.rlmin) zlcond1 = R(0.0);
+      if (warm_homo) {
+        sa_vl = sa_vl + zlcond1; sa_lv = sa_lv - zlcond1; zqxfg[QL] = zqxfg[QL] + zlcond1;
+      } else {
+        sa_vi = sa_vi + zlcond1; sa_iv = sa_iv - zlcond1; zqxfg[QI] = zqxfg[QI] + zlcond1;
+      }
+    }
+    // 3.4b(2) generation of new clouds (:1253-1363)
+    if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) {
+      real zrhc = c.ramid;
+      const real zsigk = pap_k / cc.paph_sfc;
+      if (zsigk > R(0.8)) {
+        const real s = (zsigk - R(0.8)) / R(0.2);
+        zrhc = c.ramid + (R(1.0) - c.ramid) * (s * s);
+      }
+      real zqe = R(0.0);
+      if (c.nssopt == 0 || c.nssopt == 1) {
+        zqe = (zqx[QV] - za * zqsice) / fmax(zepsec, R(1.0) - za);
+        zqe = fmax(R(0.0), zqe);
+      } else if (c.nssopt == 2) {
+        zqe = zqx[QV];
+      } else if (c.nssopt == 3) {
+        zqe = zqx[QV] + zli;
+      }
+      const real zfacn = (c.nssopt == 0 || ztp1 >= c.rtt) ? R(1.0) : zfokoop;
+      if (zqe >= zqsice * zfacn * zrhc && zqe < zqsice * zfacn) {
+        real zacond = -((R(1.0) - za) * zfacn) * zdqs / fmax(R(2.0) * (zfacn * zqsice - zqe), zepsec);
+        zacond = fmin(zacond, R(1.0) - za);
+        real zlcond2 = -(zfacn * zdqs) * R(0.5) * zacond;
+        const real zzdl = (R(2.0) * (zfacn * zqsice - zqe)) / fmax(zepsec, R(1.0) - za);
+        if (zdqs * zfacn < -zzdl) {
+          const real zlcondlim = ((za - R(1.0)) * zfacn) * zdqs - zfacn * zqsice + zqx[QV];
+          zlcond2 = fmin(zlcond2, zlcondlim);
+        }
+        zlcond2 = fmax(zlcond2, R(0.0));
+        if (R(1.0) - za < zepsec || zlcond2 < c.rlmin) {
+          zlcond2 = R(0.0);
+          zacond = R(0.0);
+        }
+        if (zlcond2 == R(0.0)) zacond = R(0.0);
+        zsolac = zsolac + zacond;
+        if (warm_homo) {
+          sa_vl = sa_vl + zlcond2; sa_lv = sa_lv - zlcond2; zqxfg[QL] = zqxfg[QL] + zlcond2;
+        } else {
+          sa_vi = sa_vi + zlcond2; sa_iv = sa_iv - zlcond2; zqxfg[QI] = zqxfg[QI] + zlcond2;
+        }
+      }
+    }
+
+    // 3.7 growth of ice by vapour deposition, Rotstayn (:1382-1447)
+    if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
+    else cs.zcldtopdist = cs.zcldtopdist + zdp / (zrho * c.rg);
+    if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
+      const real zvpice = ((c.r2es * e_ice) * c.rv) / c.rd;
+      const real zvpliq = zvpice * zfokoop;
+      const real zicenuclei = R(1000.0) * exp((R(12.96) * (zvpliq - zvpice)) / zvpliq - R(0.639));
+      const real zadd = (c.rlstt * (c.rlstt / (c.rv * ztp1) - R(1.0))) / (R(0.024) * ztp1);
+      const real zbdd = ((c.rv * ztp1) * pap_k) / (R(2.21) * zvpice);
+      const real zcvds = ((R(7.8) * pow(zicenuclei / zrho, R(0.666))) * (zvpliq - zvpice)) / ((R(8.87) * (zadd + zbdd)) * zvpice);
+      const real zice0 = fmax(zicecld, (zicenuclei * c.riceinit) / zrho);
+      const real zinew = pow((R(0.666) * zcvds) * c.ptsphy + pow(zice0, R(0.666)), R(1.5));
+      real zdepos = fmax(za * (zinew - zice0), R(0.0));
+      zdepos = fmin(zdepos, zqxfg[QL]);
+      const real zinfactor = fmin(zicenuclei / R(15000.0), R(1.0));
+      zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cs.zcldtopdist / c.rdepliqrefdepth), R(1.0));
+      sa_li = sa_li + zdepos; sa_il = sa_il - zdepos;
+      zqxfg[QI] = zqxfg[QI] + zdepos; zqxfg[QL] = zqxfg[QL] - zdepos;
+    }
+
+    // 4. revise in-cloud condensate (:1528-1533)
+    ztmpa = R(1.0) / fmax(za, zepsec);
+    zliqcld = zqxfg[QL] * ztmpa;
+    zicecld = zqxfg[QI] * ztmpa;
+    zlicld = zliqcld + zicecld;
+
+    // 4.2 sedimentation of ice, rain, snow (:1541-1576)
+    if (k > ncldtop0) {
+      fsrc_i = cs.pfx_i * zdtgdp; sa_ii = sa_ii + fsrc_i; zqxfg[QI] = zqxfg[QI] + fsrc_i; zqpretot = zqpretot + zqxfg[QI];
+      fsrc_r = cs.pfx_r * zdtgdp; sa_rr = sa_rr + fsrc_r; zqxfg[QR] = zqxfg[QR] + fsrc_r; zqpretot = zqpretot + zqxfg[QR];
+      fsrc_s = cs.pfx_s * zdtgdp; sa_ss = sa_ss + fsrc_s; zqxfg[QS] = zqxfg[QS] + fsrc_s; zqpretot = zqpretot + zqxfg[QS];
+    }
+    const real vqx_i = c.laericesed ? R(0.002) * in.pre_ice : c.rvice;
+    const real fsink_i = zdtgdp * (vqx_i * zrho);
+    const real fsink_r = zdtgdp * (c.rvrain * zrho);
+    const real fsink_s = zdtgdp * (c.rvsnow * zrho);
+
+    // precip cover overlap, MAX-RAN (:1594-1611)
+    real zcovpclr, zraincld, zsnowcld;
+    if (zqpretot > zepsec) {
+      cs.zcovptot = R(1.0) - (R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)) / (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6)));
+      cs.zcovptot = fmax(cs.zcovptot, c.rcovpmin);
+      zcovpclr = fmax(R(0.0), cs.zcovptot - za);
+      zraincld = zqxfg[QR] / cs.zcovptot;
+      zsnowcld = zqxfg[QS] / cs.zcovptot;
+      cs.zcovpmax = fmax(cs.zcovptot, cs.zcovpmax);
+    } else {
+      zraincld = R(0.0); zsnowcld = R(0.0); cs.zcovptot = R(0.0); zcovpclr = R(0.0); cs.zcovpmax = R(0.0);
+    }
+
+    const bool cold = ztp1 <= c.rtt;
+    // 4.3a autoconversion to snow (:1616-1637)
+    if (cold && zicecld > zepsec) {
+      real zzco = c.zzco_snow * exp(c.rsnowlin2 * (ztp1 - c.rtt));
+      real zlcrit = c.rlcritsnow;
+      if (c.laericeauto) {
+        zlcrit = in.picrit_aer;
+        zzco = zzco * pow(c.rnice / in.pnice, R(0.333));
+      }
+      const real r = zicecld / zlcrit;
+      sb_is = sb_is + zzco * (R(1.0) - exp(-(r * r)));
+    }
+    // 4.3b warm rain, Khairoutdinov and Kogan 2000 (:1644-1761)
+    if (zliqcld > zepsec) {
+      real zrainaut = R(0.0), zrainacc = R(0.0);
+      if (zliqcld > cc.kk_lcrit) {
+        zrainaut = ((((R(1.5) * za) * c.ptsphy) * c.rcl_kkaau) * pow(zliqcld, c.rcl_kkbauq)) * cc.kk_pow;
+        zrainaut = fmin(zrainaut, zqxfg[QL]);
+        if (zrainaut < zepsec) zrainaut = R(0.0);
+        zrainacc = (((R(2.0) * za) * c.ptsphy) * c.rcl_kkaac) * pow(zliqcld * zraincld, c.rcl_kkbac);
+        zrainacc = fmin(zrainacc, zqxfg[QL]);
+        if (zrainacc < zepsec) zrainacc = R(0.0);
+      }
+      if (cold) {
+        sa_ls = sa_ls + zrainaut; sa_ls = sa_ls + zrainacc;
+        sa_sl = sa_sl - zrainaut; sa_sl = sa_sl - zrainacc;
+      } else {
+        sa_lr = sa_lr + zrainaut; sa_lr = sa_lr + zrainacc;
+        sa_rl = sa_rl - zrainaut; sa_rl = sa_rl - zrainacc;
+      }
+    }
+    // riming of snow by cloud water (:1768-1808)
+    if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) {
+      const real zfallcorr = pow(c.rdensref / zrho, R(0.4));
+      real zsnowrime = ((((R(0.3) * cs.zcovptot) * c.ptsphy) * c.rcl_const7s) * zfallcorr) *
+                       pow((zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
+      zsnowrime = fmin(zsnowrime, R(1.0));
+      sb_ls = sb_ls + zsnowrime;
+    }
+
+    // 4.4a melting of snow and ice (:1817-1859)
+    const real zicetot = zqxfg[QI] + zqxfg[QS];
+    if (zicetot > zepsec && ztp1 > c.rtt) {
+      const real zsubsat = fmax(zqsice - zqx[QV], R(0.0));
+      const real ztdmtw0 = ztp1 - c.rtt - zsubsat * (ztw1 + ztw2 * (pap_k - ztw3) - ztw4 * (ztp1 - ztw5));
+      const real zcons1 = fabs((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)) / c.rtaumel);
+      const real zmeltmax = fmax((ztdmtw0 * zcons1) * c.zrldcp, R(0.0));
+      if (zmeltmax > zepsec) {
+        {   // ice -> rain
+          const real zalfa = zqxfg[QI] / zicetot;
+          const real zmelt = fmin(zqxfg[QI], zalfa * zmeltmax);
+          zqxfg[QI] = zqxfg[QI] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
+          sa_ir = sa_ir + zmelt; sa_ri = sa_ri - zmelt;
+        }
+        {   // snow -> rain
+          const real zalfa = zqxfg[QS] / zicetot;
+          const real zmelt = fmin(zqxfg[QS], zalfa * zmeltmax);
+          zqxfg[QS] = zqxfg[QS] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
+          sa_sr = sa_sr + zmelt; sa_rs = sa_rs - zmelt;
+        }
+      }
+    }
+
+    // 4.4b freezing of rain (:1864-1908)
+    if (zqx[QR] > zepsec) {
+      if (cold && cs.t_prev > c.rtt) {
+        const real tot = fmax(zqx[QS] + zqx[QR], zepsec);
+        cs.rainfrac = zqx[QR] / tot;
+      }
+      if (ztp1 < c.rtt) {
+        real zfrzmax;
+        if (cs.rainfrac > R(0.8)) {
+          const real zlambda = pow(c.rcl_fac1 / (zrho * zqx[QR]), c.rcl_fac2);
+          const real ztemp = c.rcl_fzrab * (ztp1 - c.rtt);
+          const real zfrz = ((c.ptsphy * (c.rcl_const5r / zrho)) * (exp(ztemp) - R(1.0))) * pow(zlambda, c.rcl_const6r);
+          zfrzmax = fmax(zfrz, R(0.0));
+        } else {
+          const real zcons1 = fabs((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))) / c.rtaumel);
+          zfrzmax = fmax(((c.rtt - ztp1) * zcons1) * c.zrldcp, R(0.0));
+        }
+        if (zfrzmax > zepsec) {
+          const real zfrz = fmin(zqx[QR], zfrzmax);
+          sa_rs = sa_rs + zfrz; sa_sr = sa_sr - zfrz;
+        }
+      }
+    }
+    // 4.4c freezing of liquid (:1913-1928)
+    {
+      const real zfrzmax = fmax((c.rthomo - ztp1) * c.zrldcp, R(0.0));
+      if (zfrzmax > zepsec && zqxfg[QL] > zepsec) {
+        const real zfrz = fmin(zqxfg[QL], zfrzmax);
+        sa_li = sa_li + zfrz; sa_il = sa_il - zfrz;
+      }
+    }
+
+    // 4.5 evaporation of rain, Abel and Boutle (:1982-2040)
+    const real zzrh0 = fmin(fmax(c.rprecrhmax + ((R(1.0) - c.rprecrhmax) * cs.zcovpmax) / fmax(zepsec, R(1.0) - za),
+                                 c.rprecrhmax), R(1.0));
+    {
+      const real zzrh = fmin(R(0.8), zzrh0);
+      const real zqe = fmax(R(0.0), fmin(zqx[QV], zqsliq));
+      if (zcovpclr > zepsec && zqxfg[QR] > zepsec && zqe < zzrh * zqsliq) {
+        const real zpreclr = zqxfg[QR] / cs.zcovptot;
+        const real zfallcorr = pow(c.rdensref / zrho, R(0.4));
+        const real zesatliq = c.rv_rd * (c.r2es * e_liq);
+        const real zlambda = pow(c.rcl_fac1 / (zrho * zpreclr), c.rcl_fac2);
+        const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * pow(ztp1, R(3.0))) * pap_k;
+        const real zcorr2 = (pow(ztp1 / R(273.0), R(1.5)) * R(393.0)) / (ztp1 + R(120.0));
+        const real zsubsat = fmax(zzrh * zqsliq - zqe, R(0.0));
+        const real zbeta = ((((R(0.5) / zqsliq) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (zcorr2 / zevap_denom) *
+                           (R(0.78) / pow(zlambda, c.rcl_const4r) + (c.rcl_const2r * sqrt(zrho * zfallcorr)) / (sqrt(zcorr2) * pow(zlambda, c.rcl_const3r)));
+        const real zdenom = R(1.0) + zbeta * c.ptsphy;
+        const real zdpevap = (((zcovpclr * zbeta) * c.ptsphy) * zsubsat) / zdenom;
+        const real zevap = fmin(zdpevap, zqxfg[QR]);
+        sa_rv = sa_rv + zevap; sa_vr = sa_vr - zevap;
+        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), ((cs.zcovptot - za) * zevap) / zqxfg[QR]));
+        zqxfg[QR] = zqxfg[QR] - zevap;
+      }
+    }
+    // 4.5 evaporation of snow, Sundqvist (:2048-2087)
+    {
+      const real zzrh = zzrh0;
+      real zqe = (zqx[QV] - za * zqsice) / fmax(zepsec, R(1.0) - za);
+      zqe = fmax(R(0.0), fmin(zqe, zqsice));
+      if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) {
+        const real x = cs.zcovptot * zdtgdp;
+        const real zpreclr = (zqxfg[QS] * zcovpclr) / copysign(fmax(fabs(x), zepsilon), x);
+        const real zbeta1 = ((sqrt(pap_k / cc.paph_sfc) / c.rvrfactor) * zpreclr) / fmax(zcovpclr, zepsec);
+        const real zbeta = c.rg_rpecons * pow(zbeta1, R(0.5777));
+        const real zdenom = R(1.0) + (zbeta * c.ptsphy) * zcorqsice;
+        const real zdpr = ((((zcovpclr * zbeta) * (zqsice - zqe)) / zdenom) * zdp) * c.zrg_r;
+        const real zdpevap = zdpr * zdtgdp;
+        const real zevap = fmin(zdpevap, zqxfg[QS]);
+        sa_sv = sa_sv + zevap; sa_vs = sa_vs - zevap;
+        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), ((cs.zcovptot - za) * zevap) / zqxfg[QS]));
+        zqxfg[QS] = zqxfg[QS] - zevap;
+      }
+    }
+    // evaporate small precipitation amounts (:2144-2158)
+    if (zqxfg[QR] < c.rlmin) { sa_rv = sa_rv + zqxfg[QR]; sa_vr = sa_vr - zqxfg[QR]; }
+    if (zqxfg[QS] < c.rlmin) { sa_sv = sa_sv + zqxfg[QS]; sa_vs = sa_vs - zqxfg[QS]; }
+
+    // 5.1 cloud cover (:2168-2180)
+    real zanew = (za + zsolac) / (R(1.0) + zsolab);
+    zanew = fmin(zanew, R(1.0));
+    if (zanew < c.ramin) zanew = R(0.0);
+    const real zda = zanew - zaorig;
+    cs.zanewm1 = zanew;
+
+    // 5.2 truncate explicit sinks, species in order (:2233-2286).
+    // Column m of zsolqa (zsolqa[n][m], n=0..4) in C indexing; for each m the
+    // sum runs n = ql, qi, qr, qs, qv and every negative entry scales
+    // zsolqa[n][m] and its transpose zsolqa[m][n] (the diagonal twice).
+    // The structurally-zero entries are kept as literal zeros so the
+    // summation order (and hence rounding) matches the dense reference.
+    {
+      real z = R(0.0), psum, zrat;
+      // m = ql: zsolqa[n][ql] = {ll, il, rl, sl, vl}
+      psum = R(0.0) + sa_ll; psum = psum + sa_il; psum = psum + sa_rl; psum = psum + sa_sl; psum = psum + sa_vl;
+      { const real zmm = fmax(zqx[QL], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      if (sa_ll < R(0.0)) { sa_ll = sa_ll * zrat; sa_ll = sa_ll * zrat; }
+      if (sa_il < R(0.0)) { sa_il = sa_il * zrat; sa_li = sa_li * zrat; }
+      if (sa_rl < R(0.0)) { sa_rl = sa_rl * zrat; sa_lr = sa_lr * zrat; }
+      if (sa_sl < R(0.0)) { sa_sl = sa_sl * zrat; sa_ls = sa_ls * zrat; }
+      if (sa_vl < R(0.0)) { sa_vl = sa_vl * zrat; sa_lv = sa_lv * zrat; }
+      // m = qi: {li, ii, ri, si(0), vi}
+      psum = R(0.0) + sa_li; psum = psum + sa_ii; psum = psum + sa_ri; psum = psum + z; psum = psum + sa_vi;
+      { const real zmm = fmax(zqx[QI], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      if (sa_li < R(0.0)) { sa_li = sa_li * zrat; sa_il = sa_il * zrat; }
+      if (sa_ii < R(0.0)) { sa_ii = sa_ii * zrat; sa_ii = sa_ii * zrat; }
+      if (sa_ri < R(0.0)) { sa_ri = sa_ri * zrat; sa_ir = sa_ir * zrat; }
+      if (sa_vi < R(0.0)) { sa_vi = sa_vi * zrat; sa_iv = sa_iv * zrat; }
+      // m = qr: {lr, ir, rr, sr, vr}
+      psum = R(0.0) + sa_lr; psum = psum + sa_ir; psum = psum + sa_rr; psum = psum + sa_sr; psum = psum + sa_vr;
+      { const real zmm = fmax(zqx[QR], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      if (sa_lr < R(0.0)) { sa_lr = sa_lr * zrat; sa_rl = sa_rl * zrat; }
+      if (sa_ir < R(0.0)) { sa_ir = sa_ir * zrat; sa_ri = sa_ri * zrat; }
+      if (sa_rr < R(0.0)) { sa_rr = sa_rr * zrat; sa_rr = sa_rr * zrat; }
+      if (sa_sr < R(0.0)) { sa_sr = sa_sr * zrat; sa_rs = sa_rs * zrat; }
+      if (sa_vr < R(0.0)) { sa_vr = sa_vr * zrat; sa_rv = sa_rv * zrat; }
+      // m = qs: {ls, is(0), rs, ss, vs}
+      psum = R(0.0) + sa_ls; psum = psum + z; psum = psum + sa_rs; psum = psum + sa_ss; psum = psum + sa_vs;
+      { const real zmm = fmax(zqx[QS], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      if (sa_ls < R(0.0)) { sa_ls = sa_ls * zrat; sa_sl = sa_sl * zrat; }
+      if (sa_rs < R(0.0)) { sa_rs = sa_rs * zrat; sa_sr = sa_sr * zrat; }
+      if (sa_ss < R(0.0)) { sa_ss = sa_ss * zrat; sa_ss = sa_ss * zrat; }
+      if (sa_vs < R(0.0)) { sa_vs = sa_vs * zrat; sa_sv = sa_sv * zrat; }
+      // m = qv: {lv, iv, rv, sv, vv(0)}
+      psum = R(0.0) + sa_lv; psum = psum + sa_iv; psum = psum + sa_rv; psum = psum + sa_sv; psum = psum + z;
+      { const real zmm = fmax(zqx[QV], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      if (sa_lv < R(0.0)) { sa_lv = sa_lv * zrat; sa_vl = sa_vl * zrat; }
+      if (sa_iv < R(0.0)) { sa_iv = sa_iv * zrat; sa_vi = sa_vi * zrat; }
+      if (sa_rv < R(0.0)) { sa_rv = sa_rv * zrat; sa_vr = sa_vr * zrat; }
+      if (sa_sv < R(0.0)) { sa_sv = sa_sv * zrat; sa_vs = sa_vs * zrat; }
+    }
+
+    // 5.2.2 implicit solver (:2294-2397).  With the zsolqb sparsity above,
+    //   zqlhs = I + diag(fallsink) + diag(row sums of zsolqb) - offdiag(zsolqb)
+    // has off-diagonal entries only at [ql][qs] and [qi][qs] (C indexing), so
+    // the unpivoted LU leaves every multiplier but those two at (signed) zero
+    // and the forward/back substitutions reduce to the terms below.  The
+    // skipped updates are x - (+/-0)*y == x exactly, so the results are
+    // bit-identical to the dense elimination for finite data.
+    {
+      // RHS: zqxn[m] = zqx[m] + sum_n zsolqa[n][m], n ascending from 0.0
+      real ex;
+      ex = R(0.0) + sa_ll; ex = ex + sa_il; ex = ex + sa_rl; ex = ex + sa_sl; ex = ex + sa_vl;
+      real qn_l = zqx[QL] + ex;
+      ex = R(0.0) + sa_li; ex = ex + sa_ii; ex = ex + sa_ri; ex = ex + R(0.0); ex = ex + sa_vi;
+      real qn_i = zqx[QI] + ex;
+      ex = R(0.0) + sa_lr; ex = ex + sa_ir; ex = ex + sa_rr; ex = ex + sa_sr; ex = ex + sa_vr;
+      real qn_r = zqx[QR] + ex;
+      ex = R(0.0) + sa_ls; ex = ex + R(0.0); ex = ex + sa_rs; ex = ex + sa_ss; ex = ex + sa_vs;
+      real qn_s = zqx[QS] + ex;
+      ex = R(0.0) + sa_lv; ex = ex + sa_iv; ex = ex + sa_rv; ex = ex + sa_sv; ex = ex + R(0.0);
+      real qn_v = zqx[QV] + ex;
+      // LHS diagonal: 1 + fallsink + sum_o zsolqb[m][o] (o ascending)
+      real d_l = R(1.0) + R(0.0);
+      d_l = d_l + sb_ll; d_l = d_l + R(0.0); d_l = d_l + R(0.0); d_l = d_l + sb_ls; d_l = d_l + R(0.0);
+      real d_i = R(1.0) + fsink_i;
+      d_i = d_i + R(0.0); d_i = d_i + sb_ii; d_i = d_i + R(0.0); d_i = d_i + sb_is; d_i = d_i + R(0.0);
+      const real d_r = R(1.0) + fsink_r;   // + five zeros
+      const real d_s = R(1.0) + fsink_s;
+      // off-diagonals zqlhs[ql][qs] = -sb_ls, zqlhs[qi][qs] = -sb_is; LU scales row-wise by
+      // the pivot of the eliminating column: zqlhs[n][m] /= zqlhs[n][n] for m > n.
+      const real u_ls = (-sb_ls) / d_l;    // zqlhs[ql][qs] after jn = ql
+      const real u_is = (-sb_is) / d_i;    // zqlhs[qi][qs] after jn = qi
+      // forward substitution (step 1): zqxn[qs] -= zqlhs[ql][qs]*zqxn[ql] + zqlhs[qi][qs]*zqxn[qi]
+      qn_s = qn_s - u_ls * qn_l;
+      qn_s = qn_s - u_is * qn_i;
+      // back substitution (step 2): vapour and the diagonal solves
+      qn_v = qn_v / R(1.0);
+      qn_s = qn_s / d_s;
+      qn_r = qn_r / d_r;
+      qn_i = qn_i / d_i;
+      qn_l = qn_l / d_l;
+      // no small values (:2402-2412)
+      if (qn_l < zepsec) { qn_v = qn_v + qn_l; qn_l = R(0.0); }
+      if (qn_i < zepsec) { qn_v = qn_v + qn_i; qn_i = R(0.0); }
+      if (qn_r < zepsec) { qn_v = qn_v + qn_r; qn_r = R(0.0); }
+      if (qn_s < zepsec) { qn_v = qn_v + qn_s; qn_s = R(0.0); }
+      zqxn[QL] = qn_l; zqxn[QI] = qn_i; zqxn[QR] = qn_r; zqxn[QS] = qn_s;
+      cs.qxnm1_l = qn_l; cs.qxnm1_i = qn_i;
+
+      // 5.3 precipitation fluxes to the next level (:2430-2448)
+      cs.pfx_i = (fsink_i * qn_i) * zrdtgdp;
+      cs.pfx_r = (fsink_r * qn_r) * zrdtgdp;
+      cs.pfx_s = (fsink_s * qn_s) * zrdtgdp;
+      if (cs.pfx_s + cs.pfx_r < zepsec) cs.zcovptot = R(0.0);
+
+      // 6. tendencies (:2456-2506)
+      {
+        const real fq_l = psup_l + conv_src_l + R(0.0) - (R(0.0) + conv_sink) * qn_l;
+        ttend = ttend + (c.ralvdcp * (qn_l - zqx[QL] - fq_l)) * c.zqtmst;
+        const real fq_i = psup_i + conv_src_i + fsrc_i - (fsink_i + conv_sink) * qn_i;
+        ttend = ttend + (c.ralsdcp * (qn_i - zqx[QI] - fq_i)) * c.zqtmst;
+        const real fq_r = R(0.0) + R(0.0) + fsrc_r - (fsink_r + R(0.0)) * qn_r;
+        ttend = ttend + (c.ralvdcp * (qn_r - zqx[QR] - fq_r)) * c.zqtmst;
+        const real fq_s = R(0.0) + R(0.0) + fsrc_s - (fsink_s + R(0.0)) * qn_s;
+        ttend = ttend + (c.ralsdcp * (qn_s - zqx[QS] - fq_s)) * c.zqtmst;
+      }
+  #pragma unroll
+      for (int m = 0; m < 4; m++) ctend[m] = R(0.0) + (zqxn[m] - zqx0[m]) * c.zqtmst;
+      qtend = qtend + (qn_v - zqx[QV]) * c.zqtmst;
+      atend = R(0.0) + zda * c.zqtmst;
+      po.zcovptot_out = cs.zcovptot;
+    }
+}
+
+// ===== 8. flux diagnostics of one level (cloudsc_c.c:2521-2582), written at half level k+1 =====
+template <typename real>
+__device__ __forceinline__ void flux_level(const DevParams<real>& c, const KArgs<real>& A, size_t h, unsigned lo,
+                                           const LevelIn<real>& in, const LevelState<real>& ls,
+                                           const PhysOut<real>& po, real paph_k, real paph_n,
+                                           CarryState<real>& cs) {
+  const real zgdph_r = -c.zrg_r * (paph_n - paph_k) * c.zqtmst;
+  const real lf = cs.fl_lf, fi = cs.fl_if, lng = cs.fl_lng, nng = cs.fl_nng;
+  const real* zqxn = po.zqxn;
+  const real* zqx0 = ls.zqx0;
+  const real* zlneg = ls.zlneg;
+  const real plude_k = po.plude_k, zfoealfa = ls.zfoealfa;
+  cs.fl_lf = lf + (zqxn[QL] - zqx0[QL] + in.pvfl * c.ptsphy - zfoealfa * plude_k) * zgdph_r;
+  cs.fl_lng = lng + zlneg[QL] * zgdph_r;
+  cs.fl_ltur = cs.fl_ltur + (in.pvfl * c.ptsphy) * zgdph_r;
+  const real rf = lf + (zqxn[QR] - zqx0[QR]) * zgdph_r;
+  const real rng = lng + zlneg[QR] * zgdph_r;
+  cs.fl_if = fi + (zqxn[QI] - zqx0[QI] + in.pvfi * c.ptsphy - (R(1.0) - zfoealfa) * plude_k) * zgdph_r;
+  cs.fl_nng = nng + zlneg[QI] * zgdph_r;
+  cs.fl_itur = cs.fl_itur + (in.pvfi * c.ptsphy) * zgdph_r;
+  const real sf = fi + (zqxn[QS] - zqx0[QS]) * zgdph_r;
+  const real sng = nng + zlneg[QS] * zgdph_r;
+  stg(A.pfsqlf, h, lo, cs.fl_lf); stg(A.pfsqif, h, lo, cs.fl_if);
+  stg(A.pfcqlng, h, lo, cs.fl_lng); stg(A.pfcqnng, h, lo, cs.fl_nng);
+  stg(A.pfsqltur, h, lo, cs.fl_ltur); stg(A.pfsqitur, h, lo, cs.fl_itur);
+  stg(A.pfsqrf, h, lo, rf); stg(A.pfcqrng, h, lo, rng); stg(A.pfsqsf, h, lo, sf); stg(A.pfcqsng, h, lo, sng);
+  const real plsl = cs.pfx_r + R(0.0);      // zpfplsx[qr] + zpfplsx[ql] (ql flux is +0)
+  const real plsn = cs.pfx_s + cs.pfx_i;
+  stg(A.pfplsl, h, lo, plsl); stg(A.pfplsn, h, lo, plsn);
+  stg(A.pfhpsl, h, lo, -c.rlvtt * plsl); stg(A.pfhpsn, h, lo, -c.rlstt * plsn);
+}
+
+// level-0 half-level outputs (cloudsc_c.c:2523-2543, 2578-2579)
+template <typename real>
+__device__ __forceinline__ void flux_top(const DevParams<real>& c, const KArgs<real>& A, size_t h0, unsigned lo) {
+  stg(A.pfsqlf, h0, lo, R(0.0)); stg(A.pfsqif, h0, lo, R(0.0)); stg(A.pfsqrf, h0, lo, R(0.0));
+  stg(A.pfsqsf, h0, lo, R(0.0)); stg(A.pfcqlng, h0, lo, R(0.0)); stg(A.pfcqnng, h0, lo, R(0.0));
+  stg(A.pfcqrng, h0, lo, R(0.0)); stg(A.pfcqsng, h0, lo, R(0.0));
+  stg(A.pfsqltur, h0, lo, R(0.0)); stg(A.pfsqitur, h0, lo, R(0.0));
+  const real plsl = R(0.0) + R(0.0), plsn = R(0.0) + R(0.0);
+  stg(A.pfplsl, h0, lo, plsl); stg(A.pfplsn, h0, lo, plsn);
+  stg(A.pfhpsl, h0, lo, -c.rlvtt * plsl); stg(A.pfhpsn, h0, lo, -c.rlstt * plsn);
+}
+
+template <typename real>
+__device__ __forceinline__ ColConst<real> column_constants(const DevParams<real>& c, const KArgs<real>& A,
+                                                           size_t u1, size_t uh, unsigned lo) {
+  ColConst<real> cc;
+  const real plsm = ldg(A.plsm, u1, lo);
+  cc.ktype = ldg(A.ktype, u1, lo * (unsigned)(sizeof(int)) / (unsigned)sizeof(real));
+  cc.paph_sfc = ldg(A.paph, uh + (size_t)A.klev * A.nproma, lo);
+  const bool land = plsm > R(0.5);
+  cc.kk_const = land ? c.rcl_kk_cloud_num_land : c.rcl_kk_cloud_num_sea;
+  cc.kk_lcrit = land ? c.rclcrit_land : c.rclcrit_sea;
+  cc.kk_pow = pow(cc.kk_const, c.rcl_kkbaun);   // loop-invariant factor of the KK autoconversion (:1721)
+  return cc;
+}
+
+template <typename real>
+__device__ __forceinline__ void store_level(const KArgs<real>& A, size_t u2, size_t u3, int k, int klev,
+                                            int nproma, unsigned lo, bool physics, const LevelState<real>& ls,
+                                            const PhysOut<real>& po) {
+  const size_t i = u2 + (size_t)k * nproma;
+  stg(A.tlt, i, lo, ls.ttend);
+  stg(A.tlq, i, lo, ls.qtend);
+  stg(A.tla, i, lo, po.atend);
+  stg(A.pcovptot, i, lo, po.zcovptot_out);
+  if (physics && k < klev - 1) stg(A.plude, i, lo, po.plude_k);   // INOUT: untouched elsewhere
+#pragma unroll
+  for (int m = 0; m < 4; m++) stg(A.tlcld, u3 + ((size_t)m * klev + k) * nproma, lo, po.ctend[m]);
+  stg(A.tlcld, u3 + ((size_t)4 * klev + k) * nproma, lo, R(0.0));
+}
+
+template <typename real>
+__device__ __forceinline__ void init_carry(CarryState<real>& cs) {
+  cs.t_prev = cs.a_prev = cs.pap_prev = R(0.0);
+  cs.zanewm1 = cs.zcovptot = cs.zcovpmax = cs.zcldtopdist = cs.rainfrac = R(0.0);
+  cs.qxnm1_l = cs.qxnm1_i = R(0.0);
+  cs.pfx_i = cs.pfx_r = cs.pfx_s = R(0.0);
+  cs.fl_lf = cs.fl_if = cs.fl_lng = cs.fl_nng = cs.fl_ltur = cs.fl_itur = R(0.0);
+}
+
+// ===================== SCC-k-caching kernel body =====================
+// `ka` points at the kernel's KArgs in the kernarg segment and `cpar` at the
+// __constant__ parameter block, both in the constant address space; they are
+// re-laundered every level so that scalar loads are issued where needed.
+template <typename real>
+__device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar) {
+  const KArgs<real>& A0 = *(const KArgs<real>*)ka;
+  const int nproma = A0.nproma, klev = A0.klev;
+  const int b = blockIdx.x, jl = threadIdx.x;
+  if (jl >= nproma || b * nproma + jl >= A0.ngptot) return;
+  const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);       // lane byte offset
+  const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
+  const size_t u2 = (size_t)b * klev * nproma;                     // [nblocks][klev][nproma]
+  const size_t uh = (size_t)b * (klev + 1) * nproma;               // [nblocks][klev+1][nproma]
+  const size_t u3 = (size_t)b * 5 * klev * nproma;                 // [nblocks][5][klev][nproma]
+
+  ColConst<real> cc;
+  CarryState<real> cs;
+  Neighbors<real> nb;
+  LevelIn<real> cur, nxt;
+  int ncldtop0;
+  {
+    const DevParams<real>& c = *(const DevParams<real>*)cpar;
+    const KArgs<real>& A = A0;
+    ncldtop0 = c.ncldtop - 1;
+    cc = column_constants(c, A, u1, uh, lo);
+    init_carry(cs);
+    flux_top(c, A, uh, lo);
+    nb.paph_k = ldg(A.paph, uh, lo);
+    nb.paph_n = ldg(A.paph, uh + nproma, lo);
+    nb.pmfu_k = ldg(A.pmfu, u2, lo); nb.pmfd_k = ldg(A.pmfd, u2, lo);
+    nb.pmfu_n = ldg(A.pmfu, u2 + nproma, lo); nb.pmfd_n = ldg(A.pmfd, u2 + nproma, lo);
+    nb.plu_n = ldg(A.plu, u2 + nproma, lo);
+    load_level(cur, A, c, u2, u3, 0, klev, nproma, lo, ncldtop0 <= 0);
+  }
+
+  for (int kloop = 0; kloop < klev; kloop++) {
+    // the level index is laundered too, so no per-field induction pointers are formed
+    int k = kloop;
+    asm volatile("" : "+s"(k));
+    const bool physics = k >= ncldtop0;
+    // ---- issue the loads of the next levels (software pipelining) ----
+    real paph_nn = R(0.0), pmfu_nn = R(0.0), pmfd_nn = R(0.0), plu_nn = R(0.0);
+    {
+      const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
+      const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar);
+      if (k + 1 < klev) {
+        load_level(nxt, A, c, u2, u3, k + 1, klev, nproma, lo, k + 1 >= ncldtop0);
+        paph_nn = ldg(A.paph, uh + (size_t)(k + 2) * nproma, lo);
+        if (k + 2 < klev) {
+          const size_t i2 = u2 + (size_t)(k + 2) * nproma;
+          pmfu_nn = ldg(A.pmfu, i2, lo); pmfd_nn = ldg(A.pmfd, i2, lo); plu_nn = ldg(A.plu, i2, lo);
+        }
+      }
+    }
+
+    LevelState<real> ls;
+    PhysOut<real> po;
+    {
+      const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar);
+      init_level(c, cur, ls);
+#pragma unroll
+      for (int m = 0; m < 4; m++) { po.zqxn[m] = R(0.0); po.ctend[m] = R(0.0); }
+      po.plude_k = cur.plude;
+      po.atend = R(0.0);
+      po.zcovptot_out = R(0.0);
+      if (physics) physics_level(c, k, klev, ncldtop0, cur, nb, cc, ls, cs, po);
+    }
+    {
+      const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
+      const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar);
+      store_level(A, u2, u3, k, klev, nproma, lo, physics, ls, po);
+      flux_level(c, A, uh + (size_t)(k + 1) * nproma, lo, cur, ls, po, nb.paph_k, nb.paph_n, cs);
+    }
+
+    // ---- rotate carried state ----
+    cs.t_prev = ls.ztp1; cs.a_prev = ls.za; cs.pap_prev = cur.pap;
+    nb.paph_k = nb.paph_n; nb.paph_n = paph_nn;
+    nb.pmfu_k = nb.pmfu_n; nb.pmfd_k = nb.pmfd_n;
+    nb.pmfu_n = pmfu_nn; nb.pmfd_n = pmfd_nn; nb.plu_n = plu_nn;
+    cur = nxt;
+  }
+  {
+    const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
+    stg(A.prainfrac, u1, lo, cs.rainfrac);
+  }
+}
+
+}  // namespace cloudsc

@@ -1,0 +1,166 @@
+// cloudsc_scc.h -- the SCC baseline CLOUDSC kernel (BASELINE config 2):
+// NPROMA block -> workgroup, column -> lane, but organised like the reference
+// C kernel (src/cloudsc_c/cloudsc/cloudsc_c.c) as separate sweeps over the
+// levels with LEVEL-SIZED temporaries ("heap temporaries"):
+//   sweep 1  (:462-640)   initial values, tidy-up, FOEALFA for every level
+//                         -> ztp1, za, zaorig, zqx, zqx0, zlneg, ... in scratch
+//   sweep 2  (:732-2508)  physics loop, reads sweep-1 temporaries back,
+//                         writes tendencies and zqxn2d / zpfplsx to scratch
+//   sweep 3  (:2521-2582) flux diagnostics from the scratch temporaries
+// The temporaries live in HBM in the coalesced [nblocks][lev][nproma] layout of
+// the reference's hoisted variant (src/cloudsc_cuda/cloudsc/cloudsc_c_hoist.cu:454-471).
+// The per-level arithmetic is the very same code as the k-caching kernel
+// (init_level / physics_level / flux_level), so both variants give bit-identical
+// results; only the data movement differs.  It exists as the measured baseline
+// the k-caching layout is compared against.
+#pragma once
+#include "cloudsc_kcache.h"
+
+namespace cloudsc {
+
+constexpr int kSccLsPlanes = 6 + 5 + 4 + 4;   // scalars, zqx, zqx0[0..3], zlneg
+
+template <typename real>
+struct SccScratch {
+  real* ls;      // [nblocks][kSccLsPlanes][klev][nproma]: LevelState without zqx0[qv]
+  real* qxn;     // [nblocks][4][klev][nproma]: zqxn2d
+  real* pfx;     // [nblocks][3][klev+1][nproma]: zpfplsx[qi,qr,qs]
+};
+
+template <typename real>
+inline long long scc_scratch_bytes(long long nblocks, long long nproma, long long klev) {
+  return (long long)sizeof(real) * nblocks * nproma * (kSccLsPlanes * klev + 4 * klev + 3 * (klev + 1));
+}
+
+template <typename real>
+inline SccScratch<real> scc_scratch_carve(char* base, long long nblocks, long long nproma, long long klev) {
+  SccScratch<real> s;
+  s.ls = (real*)base;
+  s.qxn = s.ls + nblocks * nproma * kSccLsPlanes * klev;
+  s.pfx = s.qxn + nblocks * nproma * 4 * klev;
+  return s;
+}
+
+template <typename real>
+__device__ __forceinline__ void scc_put_ls(real* base, size_t idx, size_t plane, unsigned lo, const LevelState<real>& s) {
+  stg(base, idx + 0 * plane, lo, s.ztp1); stg(base, idx + 1 * plane, lo, s.za);
+  stg(base, idx + 2 * plane, lo, s.zaorig); stg(base, idx + 3 * plane, lo, s.zfoealfa);
+  stg(base, idx + 4 * plane, lo, s.ttend); stg(base, idx + 5 * plane, lo, s.qtend);
+#pragma unroll
+  for (int m = 0; m < 5; m++) stg(base, idx + (6 + m) * plane, lo, s.zqx[m]);
+#pragma unroll
+  for (int m = 0; m < 4; m++) stg(base, idx + (11 + m) * plane, lo, s.zqx0[m]);
+#pragma unroll
+  for (int m = 0; m < 4; m++) stg(base, idx + (15 + m) * plane, lo, s.zlneg[m]);
+}
+template <typename real>
+__device__ __forceinline__ void scc_get_ls(const real* base, size_t idx, size_t plane, unsigned lo, LevelState<real>& s) {
+  s.ztp1 = ldg(base, idx + 0 * plane, lo); s.za = ldg(base, idx + 1 * plane, lo);
+  s.zaorig = ldg(base, idx + 2 * plane, lo); s.zfoealfa = ldg(base, idx + 3 * plane, lo);
+  s.ttend = ldg(base, idx + 4 * plane, lo); s.qtend = ldg(base, idx + 5 * plane, lo);
+#pragma unroll
+  for (int m = 0; m < 5; m++) s.zqx[m] = ldg(base, idx + (6 + m) * plane, lo);
+#pragma unroll
+  for (int m = 0; m < 4; m++) s.zqx0[m] = ldg(base, idx + (11 + m) * plane, lo);
+  s.zqx0[QV] = R(0.0);   // not used after sweep 1
+#pragma unroll
+  for (int m = 0; m < 4; m++) s.zlneg[m] = ldg(base, idx + (15 + m) * plane, lo);
+}
+
+template <typename real>
+__device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const SccScratch<real> S,
+                                                 cptr<DevParams<real>> cpar) {
+  const KArgs<real>& A0 = *(const KArgs<real>*)ka;
+  const int nproma = A0.nproma, klev = A0.klev;
+  const int b = blockIdx.x, jl = threadIdx.x;
+  if (jl >= nproma || b * nproma + jl >= A0.ngptot) return;
+  const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
+  const size_t u1 = (size_t)b * nproma;
+  const size_t u2 = (size_t)b * klev * nproma;
+  const size_t uh = (size_t)b * (klev + 1) * nproma;
+  const size_t u3 = (size_t)b * 5 * klev * nproma;
+  const size_t plane = (size_t)klev * nproma;
+  const size_t ulsb = (size_t)b * kSccLsPlanes * plane;        // S.ls     [planes][klev][nproma]
+  const size_t uqxb = (size_t)b * 4 * plane;                   // S.qxn    [4][klev][nproma]
+  const size_t pstride = (size_t)(klev + 1) * nproma;
+  const size_t upfb = (size_t)b * 3 * pstride;                 // S.pfx    [3][klev+1][nproma]
+  const int ncldtop0 = ((const DevParams<real>*)cpar)->ncldtop - 1;
+#define SCC_A (*(const KArgs<real>*)launder_uniform(ka))
+#define SCC_C (*(const DevParams<real>*)launder_uniform(cpar))
+
+  // ---- sweep 1: section 1 for every level ----
+  for (int k = 0; k < klev; k++) {
+    LevelIn<real> in;
+    load_level(in, SCC_A, SCC_C, u2, u3, k, klev, nproma, lo, false);
+    LevelState<real> ls;
+    init_level(SCC_C, in, ls);
+    scc_put_ls(S.ls, ulsb + (size_t)k * nproma, plane, lo, ls);
+  }
+
+  // ---- sweep 2: physics (all levels written; physics from NCLDTOP down) ----
+  const ColConst<real> cc = column_constants(SCC_C, SCC_A, u1, uh, lo);
+  CarryState<real> cs;
+  init_carry(cs);
+#pragma unroll
+  for (int m = 0; m < 3; m++) stg(S.pfx, upfb + (size_t)m * pstride, lo, R(0.0));   // zpfplsx(:,1) = 0
+  for (int k = 0; k < klev; k++) {
+    const bool physics = k >= ncldtop0;
+    const KArgs<real>& A = SCC_A;
+    LevelIn<real> in;
+    load_level(in, A, SCC_C, u2, u3, k, klev, nproma, lo, physics);
+    LevelState<real> ls;
+    scc_get_ls((const real*)S.ls, ulsb + (size_t)k * nproma, plane, lo, ls);
+    Neighbors<real> nb;
+    nb.paph_k = ldg(A.paph, uh + (size_t)k * nproma, lo);
+    nb.paph_n = ldg(A.paph, uh + (size_t)(k + 1) * nproma, lo);
+    nb.pmfu_k = ldg(A.pmfu, u2 + (size_t)k * nproma, lo);
+    nb.pmfd_k = ldg(A.pmfd, u2 + (size_t)k * nproma, lo);
+    const bool has_next = k + 1 < klev;
+    nb.pmfu_n = has_next ? ldg(A.pmfu, u2 + (size_t)(k + 1) * nproma, lo) : R(0.0);
+    nb.pmfd_n = has_next ? ldg(A.pmfd, u2 + (size_t)(k + 1) * nproma, lo) : R(0.0);
+    nb.plu_n = has_next ? ldg(A.plu, u2 + (size_t)(k + 1) * nproma, lo) : R(0.0);
+    if (k > 0) {   // level-above temporaries read back from HBM (ztp1(jk-1), za(jk-1), pap(jk-1))
+      cs.t_prev = ldg((const real*)S.ls, ulsb + (size_t)(k - 1) * nproma + 0 * plane, lo);
+      cs.a_prev = ldg((const real*)S.ls, ulsb + (size_t)(k - 1) * nproma + 1 * plane, lo);
+      cs.pap_prev = ldg(A.pap, u2 + (size_t)(k - 1) * nproma, lo);
+    }
+    PhysOut<real> po;
+#pragma unroll
+    for (int m = 0; m < 4; m++) { po.zqxn[m] = R(0.0); po.ctend[m] = R(0.0); }
+    po.plude_k = in.plude;
+    po.atend = R(0.0);
+    po.zcovptot_out = R(0.0);
+    if (physics) physics_level(SCC_C, k, klev, ncldtop0, in, nb, cc, ls, cs, po);
+    store_level(SCC_A, u2, u3, k, klev, nproma, lo, physics, ls, po);
+#pragma unroll
+    for (int m = 0; m < 4; m++) stg(S.qxn, uqxb + (size_t)m * plane + (size_t)k * nproma, lo, po.zqxn[m]);
+    stg(S.pfx, upfb + 0 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_i);
+    stg(S.pfx, upfb + 1 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_r);
+    stg(S.pfx, upfb + 2 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_s);
+  }
+  stg(SCC_A.prainfrac, u1, lo, cs.rainfrac);
+
+  // ---- sweep 3: flux diagnostics from the stored temporaries ----
+  flux_top(SCC_C, SCC_A, uh, lo);
+  for (int k = 0; k < klev; k++) {
+    const KArgs<real>& A = SCC_A;
+    LevelIn<real> in;
+    in.pvfl = ldg(A.pvfl, u2 + (size_t)k * nproma, lo);
+    in.pvfi = ldg(A.pvfi, u2 + (size_t)k * nproma, lo);
+    LevelState<real> ls;
+    scc_get_ls((const real*)S.ls, ulsb + (size_t)k * nproma, plane, lo, ls);
+    PhysOut<real> po;
+#pragma unroll
+    for (int m = 0; m < 4; m++) po.zqxn[m] = ldg((const real*)S.qxn, uqxb + (size_t)m * plane + (size_t)k * nproma, lo);
+    po.plude_k = ldg((const real*)A.plude, u2 + (size_t)k * nproma, lo);   // final (rescaled) value
+    cs.pfx_i = ldg((const real*)S.pfx, upfb + 0 * pstride + (size_t)(k + 1) * nproma, lo);
+    cs.pfx_r = ldg((const real*)S.pfx, upfb + 1 * pstride + (size_t)(k + 1) * nproma, lo);
+    cs.pfx_s = ldg((const real*)S.pfx, upfb + 2 * pstride + (size_t)(k + 1) * nproma, lo);
+    flux_level(SCC_C, A, uh + (size_t)(k + 1) * nproma, lo, in, ls, po,
+               ldg(A.paph, uh + (size_t)k * nproma, lo), ldg(A.paph, uh + (size_t)(k + 1) * nproma, lo), cs);
+  }
+#undef SCC_A
+#undef SCC_C
+}
+
+}  // namespace cloudsc
