@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--ngptot", type=int, default=163840, help="columns per GPU")
     p.add_argument("--nproma", type=int, default=128)
     p.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
-    p.add_argument("--variant", choices=["kcache", "scc"], default="kcache")
+    p.add_argument("--variant", choices=["kseg", "kcache", "scc"], default="kseg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=65536, help="columns in the CPU baseline sample")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
@@ -81,7 +81,7 @@ def main():
         dist.init_process_group("gloo")
 
     prec = ca.FP64 if args.precision == "fp64" else ca.FP32
-    variant = ca.VARIANT_KCACHE if args.variant == "kcache" else ca.VARIANT_SCC
+    variant = {"kseg": ca.VARIANT_KSEG, "kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC}[args.variant]
     ds = ca.load_dataset()
     g = ca.GpuState(ds, args.ngptot, args.nproma, prec, device=local_rank,
                     col_offset=rank * args.ngptot)
@@ -148,7 +148,8 @@ def main():
         "data": "reference 100-column IFS state (tests/golden/cloudsc100, from the reference's data/) "
                 "expanded on the device with g % 100",
         "config": {"workload": "CLOUDSC %s, NGPTOT=%d per GPU, KLEV=%d, NPROMA=%d, %s" % (
-            "SCC-k-caching" if variant == ca.VARIANT_KCACHE else "SCC (HBM temporaries)",
+            {ca.VARIANT_KSEG: "SCC-k-caching (persistent, level-segmented)",
+             ca.VARIANT_KCACHE: "SCC-k-caching", ca.VARIANT_SCC: "SCC (HBM temporaries)"}[variant],
             args.ngptot, ds.klev, args.nproma, args.precision),
             "ngptot_per_gpu": args.ngptot, "ngptot_total": total_cols, "klev": ds.klev,
             "nproma": args.nproma, "variant": args.variant, "parallelism": "columns sharded, %d GPU(s)" % world},

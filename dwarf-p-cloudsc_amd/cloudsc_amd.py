@@ -35,7 +35,7 @@ GOLDEN_DIR = os.path.join(REPO, "tests", "golden", "cloudsc100")
 
 NCLV = 5
 FP64, FP32 = 8, 4
-VARIANT_SCC, VARIANT_KCACHE = 1, 2
+VARIANT_SCC, VARIANT_KCACHE, VARIANT_KSEG = 1, 2, 3
 
 # ---------------------------------------------------------------------------
 # cloudsc_params_t  (order == include/cloudsc_amd.h)

@@ -70,6 +70,32 @@ __device__ __forceinline__ T launder_vgpr(T v) {
 // (the JPRB=sp semantics, parkind1.F90:40-43).
 #define R(x) (real)(x)
 
+// Device math used by the kernels.  One place to swap implementations; the
+// CLOUDSC_ABLATE_* macros exist only for timing-only diagnostic builds (they
+// give wrong results) that price each function's share of the kernel.
+#ifdef CLOUDSC_NOINLINE_POW
+__device__ __attribute__((noinline)) double cl_pow_ool(double x, double y);
+__device__ __attribute__((noinline)) float cl_pow_ool(float x, float y);
+#endif
+template <typename real>
+__device__ __forceinline__ real cl_pow(real x, real y) {
+#if defined(CLOUDSC_ABLATE_POW)
+  return x * y;
+#elif defined(CLOUDSC_NOINLINE_POW)
+  return cl_pow_ool(x, y);
+#else
+  return pow(x, y);
+#endif
+}
+template <typename real>
+__device__ __forceinline__ real cl_exp(real x) {
+#ifdef CLOUDSC_ABLATE_EXP
+  return x + (real)1.0;
+#else
+  return exp(x);
+#endif
+}
+
 // FOEALFA (src/common/include/fcttre.func.h; inlined at cloudsc_c.c:588,831,1162-1174)
 template <typename real, typename P>
 __device__ __forceinline__ real foealfa(const P& c, real t) {
@@ -77,9 +103,9 @@ __device__ __forceinline__ real foealfa(const P& c, real t) {
   return fmin(R(1.0), x * x);            // pow(x,2) == x*x (both rounded once)
 }
 template <typename real, typename P>
-__device__ __forceinline__ real exp_liq(const P& c, real t) { return exp((c.r3les * (t - c.rtt)) / (t - c.r4les)); }
+__device__ __forceinline__ real exp_liq(const P& c, real t) { return cl_exp<real>((c.r3les * (t - c.rtt)) / (t - c.r4les)); }
 template <typename real, typename P>
-__device__ __forceinline__ real exp_ice(const P& c, real t) { return exp((c.r3ies * (t - c.rtt)) / (t - c.r4ies)); }
+__device__ __forceinline__ real exp_ice(const P& c, real t) { return cl_exp<real>((c.r3ies * (t - c.rtt)) / (t - c.r4ies)); }
 
 // alfa*R5ALVCP/(T-R4LES)^2 + (1-alfa)*R5ALSCP/(T-R4IES)^2 (cloudsc_c.c:1166,1220)
 template <typename real, typename P>

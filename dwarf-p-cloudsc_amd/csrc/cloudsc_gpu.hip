@@ -29,6 +29,10 @@ using namespace cloudsc;
 // ---------------------------------------------------------------------------
 // __constant__ parameter mirrors
 // ---------------------------------------------------------------------------
+#ifdef CLOUDSC_NOINLINE_POW
+__device__ __attribute__((noinline)) double cloudsc::cl_pow_ool(double x, double y) { return pow(x, y); }
+__device__ __attribute__((noinline)) float cloudsc::cl_pow_ool(float x, float y) { return pow(x, y); }
+#endif
 __constant__ DevParams<double> g_params_dp;
 __constant__ DevParams<float> g_params_sp;
 
@@ -37,6 +41,8 @@ namespace {
 thread_local char g_hip_err[256] = "";
 constexpr int kMaxDevices = 64;
 bool g_inited[kMaxDevices] = {false};
+bool g_aer[kMaxDevices] = {false};      // LAERICESED || LAERICEAUTO of the device's parameters
+int g_ncldtop[kMaxDevices] = {0};       // NCLDTOP of the device's parameters (KSEG segment bounds)
 
 int hip_fail(hipError_t e, const char* what) {
   snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s", what, hipGetErrorString(e));
@@ -149,15 +155,21 @@ template <> __device__ __forceinline__ cptr<DevParams<float>> dev_params<float>(
 // Kernel entry points.  The KArgs struct is the first explicit kernel argument,
 // i.e. it sits at offset 0 of the kernarg segment; the bodies read it (and the
 // parameter block) through constant-address-space pointers.
-template <typename real>
-__global__ void __launch_bounds__(256) kcache_entry(const KArgs<real> a) {
+template <typename real, int WAVES, int PF, bool AER>
+__global__ void __launch_bounds__(256, WAVES) kcache_entry(const KArgs<real> a) {
   (void)a;
-  cloudsc_kcache_body<real>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), dev_params<real>());
+  cloudsc_kcache_body<real, PF, AER>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), dev_params<real>());
 }
-template <typename real>
+template <typename real, int WAVES, int PF, bool AER>
+__global__ void __launch_bounds__(256, WAVES) kseg_entry(const KArgs<real> a, const PersistArgs<real> pa) {
+  (void)a;
+  cloudsc_kcache_persistent_body<real, PF, AER>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
+                                                dev_params<real>(), pa);
+}
+template <typename real, bool AER>
 __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccScratch<real> s) {
   (void)a;
-  cloudsc_scc_body<real>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), s, dev_params<real>());
+  cloudsc_scc_body<real, AER>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), s, dev_params<real>());
 }
 
 // ---------------------------------------------------------------------------
@@ -214,29 +226,142 @@ __global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld
 // ---------------------------------------------------------------------------
 namespace {
 
+template <typename real> int kcache_default_cfg();
+template <> int kcache_default_cfg<double>() { return 20; }
+template <> int kcache_default_cfg<float>() { return 31; }
+
 int validate_run_args(int device, int precision, int variant, int ngptot, int nproma, int klev) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CLOUDSC_ENODEV;
   if (device < 0 || device >= n || device >= kMaxDevices) return CLOUDSC_ENODEV;
   if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return CLOUDSC_EINVAL;
-  if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC) return CLOUDSC_EINVAL;
+  if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC && variant != CLOUDSC_VARIANT_KSEG)
+    return CLOUDSC_EINVAL;
   if (ngptot <= 0 || nproma <= 0 || nproma > 256 || klev < 2) return CLOUDSC_EINVAL;
   if (!g_inited[device]) return CLOUDSC_ENOINIT;
   return CLOUDSC_OK;
 }
 
+template <typename real, bool AER>
+int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma, int cfg) {
+  switch (cfg) {
+    case 10: hipLaunchKernelGGL((kcache_entry<real, 1, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    case 11: hipLaunchKernelGGL((kcache_entry<real, 1, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    case 20: hipLaunchKernelGGL((kcache_entry<real, 2, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    case 21: hipLaunchKernelGGL((kcache_entry<real, 2, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    case 30: hipLaunchKernelGGL((kcache_entry<real, 3, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    case 31: hipLaunchKernelGGL((kcache_entry<real, 3, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    default: return CLOUDSC_EINVAL;
+  }
+  return CLOUDSC_OK;
+}
+
+// ---- persistent segmented variant ----
+// workspace: [counter, err, pad..][flags: nblocks][carry state], 256-byte aligned parts
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+size_t kseg_ctl_bytes(int nblocks) { return align256(256 + (size_t)nblocks * sizeof(unsigned)); }
 template <typename real>
-int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
+size_t kseg_scratch_bytes(int nblocks, int nproma) {
+  return kseg_ctl_bytes(nblocks) + (size_t)nblocks * kCarryN * nproma * sizeof(real);
+}
+
+// measured (profiles/r01): fp64 2.72 ms one-shot -> 2.37 ms with 8 segments;
+// beyond 8 the tail no longer shrinks
+int kseg_nseg() {
+  int n = 8;
+  if (const char* e = getenv("CLOUDSC_KSEG_NSEG")) n = atoi(e);
+  return n < 1 ? 1 : (n > kMaxSeg ? kMaxSeg : n);
+}
+
+// segment boundaries: levels above NCLDTOP only initialise and store (cheap),
+// so the physics levels are split evenly and the first segment also takes the
+// levels above the cloud top
+void kseg_bounds(int nseg, int klev, int ncldtop, int* lev) {
+  const int top = ncldtop - 1 < klev ? (ncldtop - 1 > 0 ? ncldtop - 1 : 0) : klev;
+  const int phys = klev - top;
+  lev[0] = 0;
+  for (int sgm = 1; sgm < nseg; sgm++) lev[sgm] = top + (int)(((long long)phys * sgm + nseg / 2) / nseg);
+  lev[nseg] = klev;
+}
+
+template <typename real, int WAVES, int PF, bool AER>
+int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
+  auto kern = kseg_entry<real, WAVES, PF, AER>;
+  // one workgroup per resident slot (an over-estimate only delays the extra
+  // workgroups: progress never depends on residency, items are dequeued in order)
+  static int cache[257] = {0};
+  int& per_cu = cache[nproma];
+  if (!per_cu) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, nproma, 0) != hipSuccess || n <= 0) n = 1;
+    per_cu = n;
+  }
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  int grid = per_cu * ncu;
+  if (const char* e = getenv("CLOUDSC_KSEG_GRID")) grid = atoi(e) > 0 ? atoi(e) : grid;
+  if (grid > nitems) grid = nitems;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(nproma), 0, st, a, pa);
+  return CLOUDSC_OK;
+}
+
+template <typename real, bool AER>
+int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
+                int cfg) {
+  switch (cfg) {
+    case 10: return launch_kseg_cfg<real, 1, 0, AER>(st, a, pa, nproma, nitems);
+    case 11: return launch_kseg_cfg<real, 1, 1, AER>(st, a, pa, nproma, nitems);
+    case 20: return launch_kseg_cfg<real, 2, 0, AER>(st, a, pa, nproma, nitems);
+    case 21: return launch_kseg_cfg<real, 2, 1, AER>(st, a, pa, nproma, nitems);
+    case 30: return launch_kseg_cfg<real, 3, 0, AER>(st, a, pa, nproma, nitems);
+    case 31: return launch_kseg_cfg<real, 3, 1, AER>(st, a, pa, nproma, nitems);
+    default: return CLOUDSC_EINVAL;
+  }
+}
+
+template <typename real>
+int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
            void* scratch) {
   const KArgs<real> a = make_args<real>(f, ngptot, nproma, klev);
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  const bool aer = g_aer[device];
+  if (aer && (!f->pre_ice || !f->picrit_aer || !f->pnice)) return CLOUDSC_EINVAL;
+  int rc = CLOUDSC_OK;
   if (variant == CLOUDSC_VARIANT_KCACHE) {
-    hipLaunchKernelGGL(kcache_entry<real>, dim3(nblocks), dim3(nproma), 0, st, a);
+    // kernel configuration (occupancy target x load schedule); the default is
+    // the measured best, CLOUDSC_KCACHE_CFG=<waves><pf> overrides it for experiments
+    int cfg = kcache_default_cfg<real>();
+    if (const char* e = getenv("CLOUDSC_KCACHE_CFG")) cfg = atoi(e);
+    rc = aer ? launch_kcache<real, true>(st, a, nblocks, nproma, cfg)
+             : launch_kcache<real, false>(st, a, nblocks, nproma, cfg);
+  } else if (variant == CLOUDSC_VARIANT_KSEG) {
+    if (!scratch) return CLOUDSC_EINVAL;
+    int cfg = kcache_default_cfg<real>();
+    if (const char* e = getenv("CLOUDSC_KCACHE_CFG")) cfg = atoi(e);
+    const int ncldtop = g_ncldtop[device];
+    PersistArgs<real> pa;
+    pa.counter = (unsigned*)scratch;
+    pa.err = (unsigned*)scratch + 1;
+    pa.flags = (unsigned*)((char*)scratch + 256);
+    pa.state = (real*)((char*)scratch + kseg_ctl_bytes(nblocks));
+    pa.nseg = kseg_nseg();
+    if (pa.nseg > klev) pa.nseg = klev;
+    pa.nblocks = nblocks;
+    pa.nitems = pa.nseg * nblocks;
+    for (int q = 0; q <= kMaxSeg; q++) pa.lev[q] = klev;
+    kseg_bounds(pa.nseg, klev, ncldtop, pa.lev);
+    HIPCHK(hipMemsetAsync(scratch, 0, kseg_ctl_bytes(nblocks), st));
+    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, cfg)
+             : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, cfg);
   } else {
     if (!scratch) return CLOUDSC_EINVAL;
     SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
-    hipLaunchKernelGGL(scc_entry<real>, dim3(nblocks), dim3(nproma), 0, st, a, s);
+    if (aer) hipLaunchKernelGGL((scc_entry<real, true>), dim3(nblocks), dim3(nproma), 0, st, a, s);
+    else hipLaunchKernelGGL((scc_entry<real, false>), dim3(nblocks), dim3(nproma), 0, st, a, s);
   }
+  if (rc) return rc;
   HIPCHK(hipGetLastError());
   return CLOUDSC_OK;
 }
@@ -269,14 +394,21 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t* params) {
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_params_dp), &dp, sizeof(dp)));
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_params_sp), &sp, sizeof(sp)));
   HIPCHK(hipDeviceSynchronize());
+  g_aer[device] = params->laericesed || params->laericeauto;
+  g_ncldtop[device] = params->ncldtop;
   g_inited[device] = true;
   return CLOUDSC_OK;
 }
 
 long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev) {
-  if (variant != CLOUDSC_VARIANT_SCC) return 0;
+  if (variant == CLOUDSC_VARIANT_KCACHE) return 0;
   if (ngptot <= 0 || nproma <= 0 || klev < 2) return -1;
+  if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return -1;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  if (variant == CLOUDSC_VARIANT_KSEG)
+    return precision == CLOUDSC_FP64 ? kseg_scratch_bytes<double>(nblocks, nproma)
+                                     : kseg_scratch_bytes<float>(nblocks, nproma);
+  if (variant != CLOUDSC_VARIANT_SCC) return -1;
   return precision == CLOUDSC_FP64 ? scc_scratch_bytes<double>(nblocks, nproma, klev)
                                    : scc_scratch_bytes<float>(nblocks, nproma, klev);
 }
@@ -288,8 +420,8 @@ int cloudsc_gpu_run(int device, void* stream, int precision, int variant, int ng
   if (!f || !fields_complete(f)) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
-  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch)
-                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch);
+  return precision == CLOUDSC_FP64 ? launch<double>(device, st, variant, f, ngptot, nproma, klev, scratch)
+                                   : launch<float>(device, st, variant, f, ngptot, nproma, klev, scratch);
 }
 
 const char* cloudsc_strerror(int code) {
@@ -306,6 +438,15 @@ const char* cloudsc_strerror(int code) {
 }
 
 const char* cloudsc_last_hip_error(void) { return g_hip_err; }
+
+#ifdef CLOUDSC_KSEG_TRACE
+// diagnostic build only (tools/kseg_trace.py): per item {start, end, workgroup, xcc<<16|hw_id}
+int cloudsc_kseg_trace(unsigned long long* host, int nitems) {
+  if (nitems > kTraceMax) nitems = kTraceMax;
+  HIPCHK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_kseg_trace), sizeof(unsigned long long) * 4 * nitems));
+  return CLOUDSC_OK;
+}
+#endif
 
 long long cloudsc_abi_sizeof(int which) {
   switch (which) {
@@ -331,8 +472,8 @@ struct cloudsc_gpu_state {
   hipEvent_t ev0, ev1;
   cloudsc_fields_t f;             // device pointers
   void* plude_pristine;
-  void* scratch;
-  size_t scratch_bytes;
+  void* scratch;                  // SCC temporaries
+  void* kseg_ws;                  // KSEG counter, flags and carried state
   std::vector<void*> allocs;
 };
 
@@ -488,10 +629,16 @@ int cloudsc_state_reset(cloudsc_gpu_state_t* s) {
 int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) {
   if (!s || reps <= 0) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(s->device));
-  if (variant == CLOUDSC_VARIANT_SCC && !s->scratch) {     // SCC temporaries, allocated on first use
-    s->scratch_bytes = (size_t)cloudsc_gpu_scratch_bytes(s->precision, variant, s->ngptot, s->nproma, s->klev);
-    int rc0 = dalloc(s, &s->scratch, s->scratch_bytes);
-    if (rc0) return rc0;
+  void* scratch = nullptr;
+  if (variant == CLOUDSC_VARIANT_SCC || variant == CLOUDSC_VARIANT_KSEG) {   // workspaces, allocated on first use
+    void*& ws = variant == CLOUDSC_VARIANT_SCC ? s->scratch : s->kseg_ws;
+    if (!ws) {
+      const long long nb = cloudsc_gpu_scratch_bytes(s->precision, variant, s->ngptot, s->nproma, s->klev);
+      if (nb <= 0) return CLOUDSC_EINVAL;
+      int rc0 = dalloc(s, &ws, (size_t)nb);
+      if (rc0) return rc0;
+    }
+    scratch = ws;
   }
   std::vector<hipEvent_t> ev(2 * (size_t)reps);
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
@@ -501,7 +648,7 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     if (rc) break;
     HIPCHK(hipEventRecord(ev[2 * r], s->stream));
     rc = cloudsc_gpu_run(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f,
-                         s->scratch);
+                         scratch);
     HIPCHK(hipEventRecord(ev[2 * r + 1], s->stream));
   }
   hipError_t e = hipStreamSynchronize(s->stream);
@@ -513,6 +660,16 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     if (ms) ms[r] = t;
   }
   for (auto& x : ev) hipEventDestroy(x);
+  if (rc == CLOUDSC_OK && variant == CLOUDSC_VARIANT_KSEG) {
+    // a segment whose predecessor never arrived gives up after a bounded spin
+    // and counts itself here: its results are invalid
+    unsigned err = 0;
+    HIPCHK(hipMemcpy(&err, (unsigned*)scratch + 1, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+      std::snprintf(g_hip_err, sizeof(g_hip_err), "KSEG: %u segment hand-offs timed out", err);
+      rc = CLOUDSC_EHIP;
+    }
+  }
   return rc;
 }
 

@@ -26,6 +26,23 @@
 // last-ulp results of OCML exp/pow vs glibc.
 #pragma once
 #include "cloudsc_dev.h"
+#ifdef CLOUDSC_BRANCH_STATS
+// diagnostic build only: count the waves that enter each branch body
+__device__ unsigned long long g_branch_count[32];
+#define CLOUDSC_BRANCH_COUNT(id)                                                         \
+  do {                                                                                 \
+    const unsigned long long m_ = __ballot(1);                                         \
+    if ((int)__lane_id() == __ffsll((long long)m_) - 1) atomicAdd(&g_branch_count[id], 1ull); \
+  } while (0)
+#else
+#define CLOUDSC_BRANCH_COUNT(id) do {} while (0)
+#endif
+#ifdef CLOUDSC_CONST_PARAMS
+#include CLOUDSC_CONST_PARAMS   // experiment: parameters as compile-time constants
+#define CLOUDSC_PARAMS_HERE const ConstParams<real> c{}
+#else
+#define CLOUDSC_PARAMS_HERE const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar)
+#endif
 
 namespace cloudsc {
 
@@ -101,10 +118,12 @@ struct PhysOut {
   real plude_k, atend, ctend[4], zcovptot_out;
 };
 
-template <typename real>
-__device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& A, const DevParams<real>& c,
-                                           size_t u2, size_t u3, int k, int klev, int nproma, unsigned lo,
-                                           bool physics) {
+// All loads of a level are unconditional (the physics-only fields are read at
+// every level): branches around memory operations make hipcc's vmcnt
+// bookkeeping fall back to vmcnt(0), which drains the software pipeline.
+template <typename real, bool AER>
+__device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& A, size_t u2, size_t u3, int k,
+                                           int klev, int nproma, unsigned lo) {
   const size_t i = u2 + (size_t)k * nproma;
   L.pt = ldg(A.pt, i, lo); L.pq = ldg(A.pq, i, lo); L.ttt = ldg(A.ttt, i, lo); L.ttq = ldg(A.ttq, i, lo);
   L.tta = ldg(A.tta, i, lo); L.pa = ldg(A.pa, i, lo); L.pap = ldg(A.pap, i, lo);
@@ -115,18 +134,18 @@ __device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& 
     L.pclv[m] = ldg(A.pclv, j, lo);
     L.ttcld[m] = ldg(A.ttcld, j, lo);
   }
-  if (physics) {
-    L.phrsw = ldg(A.phrsw, i, lo); L.phrlw = ldg(A.phrlw, i, lo); L.pvervel = ldg(A.pvervel, i, lo);
-    L.psnde = ldg(A.psnde, i, lo); L.psupsat = ldg(A.psupsat, i, lo);
-    L.pre_ice = c.laericesed ? ldg(A.pre_ice, i, lo) : R(0.0);
-    L.picrit_aer = c.laericeauto ? ldg(A.picrit_aer, i, lo) : R(0.0);
-    L.pnice = c.laericeauto ? ldg(A.pnice, i, lo) : R(0.0);
+  L.phrsw = ldg(A.phrsw, i, lo); L.phrlw = ldg(A.phrlw, i, lo); L.pvervel = ldg(A.pvervel, i, lo);
+  L.psnde = ldg(A.psnde, i, lo); L.psupsat = ldg(A.psupsat, i, lo);
+  if (AER) {   // LAERICESED / LAERICEAUTO inputs; the launch picks AER from the flags
+    L.pre_ice = ldg(A.pre_ice, i, lo); L.picrit_aer = ldg(A.picrit_aer, i, lo); L.pnice = ldg(A.pnice, i, lo);
+  } else {
+    L.pre_ice = R(0.0); L.picrit_aer = R(1.0); L.pnice = R(1.0);
   }
 }
 
 // ===== 1. initial values, tidy-up, FOEALFA at one level (cloudsc_c.c:462-575, 588, 625) =====
-template <typename real>
-__device__ __forceinline__ void init_level(const DevParams<real>& c, const LevelIn<real>& in, LevelState<real>& s) {
+template <typename real, typename P>
+__device__ __forceinline__ void init_level(const P& c, const LevelIn<real>& in, LevelState<real>& s) {
   s.ztp1 = in.pt + c.ptsphy * in.ttt;
   real* zqx = s.zqx;
   real* zlneg = s.zlneg;
@@ -178,8 +197,8 @@ __device__ __forceinline__ void init_level(const DevParams<real>& c, const Level
 }
 
 // ===== 3.-6. physics of one level ncldtop <= k (cloudsc_c.c:732-2508) =====
-template <typename real>
-__device__ __forceinline__ void physics_level(const DevParams<real>& c, const int k, const int klev,
+template <typename real, typename P>
+__device__ __forceinline__ void physics_level(const P& c, const int k, const int klev,
                                               const int ncldtop0, const LevelIn<real>& in,
                                               const Neighbors<real>& nb, const ColConst<real>& cc,
                                               LevelState<real>& ls, CarryState<real>& cs, PhysOut<real>& po) {
@@ -196,6 +215,7 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
   real* ctend = po.ctend;
   real& plude_k = po.plude_k;
   real& atend = po.atend;
+  CLOUDSC_BRANCH_COUNT(31);
     const real pap_k = in.pap;
     // saturation values (:583-609)
     const real e_liq = exp_liq<real>(c, ztp1), e_ice = exp_ice<real>(c, ztp1);
@@ -219,11 +239,16 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
     real zqxfg[5];
   #pragma unroll
     for (int m = 0; m < 5; m++) zqxfg[m] = zqx[m];
-    // zsolqa is dense in the reference; the entries that can become non-zero
-    // are kept as named scalars sa_<a><b> == zsolqa[a][b] (C indexing).
-    real sa_ll = 0, sa_lv = 0, sa_vl = 0, sa_ii = 0, sa_iv = 0, sa_vi = 0, sa_ss = 0;
-    real sa_li = 0, sa_il = 0, sa_ls = 0, sa_sl = 0, sa_lr = 0, sa_rl = 0, sa_rr = 0;
-    real sa_ir = 0, sa_ri = 0, sa_sr = 0, sa_rs = 0, sa_rv = 0, sa_vr = 0, sa_sv = 0, sa_vs = 0;
+    // zsolqa is dense in the reference; only 13 entries can become non-zero
+    // here, kept as named scalars sa_<a><b> == zsolqa[a][b] (C indexing).  Every
+    // off-diagonal pair is updated antisymmetrically (x to one, -x to the other,
+    // in the same order, and scaled by the same factors in 5.2), and IEEE
+    // negation is exact and sign-symmetric under round-to-nearest, so
+    // zsolqa[b][a] == -zsolqa[a][b] exactly: only one of each pair is stored.
+    //   stored: ll ii rr ss (diagonal)  lv iv li ls lr ir sr rv sv
+    //   implied: vl=-lv vi=-iv il=-li sl=-ls rl=-lr ri=-ir rs=-sr vr=-rv vs=-sv
+    real sa_ll = 0, sa_ii = 0, sa_rr = 0, sa_ss = 0;
+    real sa_lv = 0, sa_iv = 0, sa_li = 0, sa_ls = 0, sa_lr = 0, sa_ir = 0, sa_sr = 0, sa_rv = 0, sa_sv = 0;
     // zsolqb non-zeros: [ql][ql], [qi][qi] (subsidence), [qi][qs] (snow autoconv), [ql][qs] (riming)
     real sb_ll = 0, sb_ii = 0, sb_is = 0, sb_ls = 0;
     real conv_src_l = 0, conv_src_i = 0, conv_sink = 0, psup_l = 0, psup_i = 0;
@@ -253,8 +278,8 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
     real zlicld = zliqcld + zicecld;
 
     // evaporate very small amounts of liquid and ice (:846-859)
-    if (zqx[QL] < c.rlmin) { sa_lv = zqx[QL]; sa_vl = -zqx[QL]; }
-    if (zqx[QI] < c.rlmin) { sa_iv = zqx[QI]; sa_vi = -zqx[QI]; }
+    if (zqx[QL] < c.rlmin) { sa_lv = zqx[QL]; }
+    if (zqx[QI] < c.rlmin) { sa_iv = zqx[QI]; }
 
     // 3.1 ice supersaturation adjustment (:874-954)
     const real zfokoop = fmin(c.rkoop1 - c.rkoop2 * ztp1, (c.r2es * e_liq) * R(1.0) / (c.r2es * e_ice));
@@ -273,15 +298,13 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
       zsupsat = fmax(((R(1.0) - za) * (zqp1env - zfac * zqsice)) / zcorqsice, R(0.0));
     }
     const bool warm_homo = ztp1 > c.rthomo;
-    if (zsupsat > zepsec) {
-      if (warm_homo) {
-        sa_vl = sa_vl + zsupsat; sa_lv = sa_lv - zsupsat; zqxfg[QL] = zqxfg[QL] + zsupsat;
-      } else {
-        sa_vi = sa_vi + zsupsat; sa_iv = sa_iv - zsupsat; zqxfg[QI] = zqxfg[QI] + zsupsat;
+    if (zsupsat > zepsec) { CLOUDSC_BRANCH_COUNT(0);
+      if (warm_homo) { sa_lv = sa_lv - zsupsat; zqxfg[QL] = zqxfg[QL] + zsupsat;
+      } else { sa_iv = sa_iv - zsupsat; zqxfg[QI] = zqxfg[QI] + zsupsat;
       }
       zsolac = (R(1.0) - za) * zfaci;
     }
-    if (in.psupsat > zepsec) {
+    if (in.psupsat > zepsec) { CLOUDSC_BRANCH_COUNT(1);
       if (warm_homo) {
         sa_ll = sa_ll + in.psupsat; psup_l = in.psupsat; zqxfg[QL] = zqxfg[QL] + in.psupsat;
       } else {
@@ -322,14 +345,14 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
         const real zevap = fmin(zlcust_l - zlfinal, zevaplimmix);
         zlfinal = zlcust_l - zevap;
         zlfinalsum = zlfinalsum + zlfinal;
-        sa_ll = sa_ll + zlcust_l; sa_lv = sa_lv + zevap; sa_vl = sa_vl - zevap;
+        sa_ll = sa_ll + zlcust_l; sa_lv = sa_lv + zevap;
       }
       {
         real zlfinal = fmax(R(0.0), zlcust_i - zdqs);
         const real zevap = fmin(zlcust_i - zlfinal, zevaplimmix);
         zlfinal = zlcust_i - zevap;
         zlfinalsum = zlfinalsum + zlfinal;
-        sa_ii = sa_ii + zlcust_i; sa_iv = sa_iv + zevap; sa_vi = sa_vi - zevap;
+        sa_ii = sa_ii + zlcust_i; sa_iv = sa_iv + zevap;
       }
       if (zlfinalsum < zepsec) zacust = R(0.0);
       zsolac = zsolac + zacust;
@@ -346,15 +369,15 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
 
     // 3.4 erosion of clouds by turbulent mixing (:1087-1118)
     const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? c.zldifdt_conv : c.zldifdt0;
-    if (zli > zepsec) {
+    if (zli > zepsec) { CLOUDSC_BRANCH_COUNT(2);
       const real ze = zldifdt * fmax(zqsmix - zqx[QV], R(0.0));
       real zleros = za * ze;
       zleros = fmin(zleros, zevaplimmix);
       zleros = fmin(zleros, zli);
       const real zaeros = zleros / zlicld;
       zsolac = zsolac - zaeros;
-      sa_lv = sa_lv + zliqfrac * zleros; sa_vl = sa_vl - zliqfrac * zleros;
-      sa_iv = sa_iv + zicefrac * zleros; sa_vi = sa_vi - zicefrac * zleros;
+      sa_lv = sa_lv + zliqfrac * zleros;
+      sa_iv = sa_iv + zicefrac * zleros;
     }
 
     // 3.4 condensation/evaporation due to dqsat/dt: two Newton steps (:1137-1182)
@@ -386,15 +409,15 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
     }
 
     // 3.4a evaporation of clouds (:1189-1207)
-    if (zdqs > R(0.0)) {
+    if (zdqs > R(0.0)) { CLOUDSC_BRANCH_COUNT(3);
       real zlevap = za * fmin(zdqs, zlicld);
       zlevap = fmin(zlevap, zevaplimmix);
       zlevap = fmin(zlevap, fmax(zqsmix - zqx[QV], R(0.0)));
-      sa_lv = sa_lv + zliqfrac * zlevap; sa_vl = sa_vl - zliqfrac * zlevap;
-      sa_iv = sa_iv + zicefrac * zlevap; sa_vi = sa_vi - zicefrac * zlevap;
+      sa_lv = sa_lv + zliqfrac * zlevap;
+      sa_iv = sa_iv + zicefrac * zlevap;
     }
     // 3.4b(1) increase of cloud water in existing clouds (:1213-1250)
-    if (zdqs <= -c.rlmin && za > zepsec) {
+    if (zdqs <= -c.rlmin && za > zepsec) { CLOUDSC_BRANCH_COUNT(4);
       real zlcond1 = fmax(-zdqs, R(0.0));
       real zcdmax;
       if (za > R(0.99)) {
@@ -406,14 +429,12 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
       zlcond1 = fmax(fmin(zlcond1, zcdmax), R(0.0));
       zlcond1 = za * zlcond1;
       if (zlcond1 < c.rlmin) zlcond1 = R(0.0);
-      if (warm_homo) {
-        sa_vl = sa_vl + zlcond1; sa_lv = sa_lv - zlcond1; zqxfg[QL] = zqxfg[QL] + zlcond1;
-      } else {
-        sa_vi = sa_vi + zlcond1; sa_iv = sa_iv - zlcond1; zqxfg[QI] = zqxfg[QI] + zlcond1;
+      if (warm_homo) { sa_lv = sa_lv - zlcond1; zqxfg[QL] = zqxfg[QL] + zlcond1;
+      } else { sa_iv = sa_iv - zlcond1; zqxfg[QI] = zqxfg[QI] + zlcond1;
       }
     }
     // 3.4b(2) generation of new clouds (:1253-1363)
-    if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) {
+    if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) { CLOUDSC_BRANCH_COUNT(5);
       real zrhc = c.ramid;
       const real zsigk = pap_k / cc.paph_sfc;
       if (zsigk > R(0.8)) {
@@ -430,7 +451,7 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
         zqe = zqx[QV] + zli;
       }
       const real zfacn = (c.nssopt == 0 || ztp1 >= c.rtt) ? R(1.0) : zfokoop;
-      if (zqe >= zqsice * zfacn * zrhc && zqe < zqsice * zfacn) {
+      if (zqe >= zqsice * zfacn * zrhc && zqe < zqsice * zfacn) { CLOUDSC_BRANCH_COUNT(6);
         real zacond = -((R(1.0) - za) * zfacn) * zdqs / fmax(R(2.0) * (zfacn * zqsice - zqe), zepsec);
         zacond = fmin(zacond, R(1.0) - za);
         real zlcond2 = -(zfacn * zdqs) * R(0.5) * zacond;
@@ -446,10 +467,8 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
         }
         if (zlcond2 == R(0.0)) zacond = R(0.0);
         zsolac = zsolac + zacond;
-        if (warm_homo) {
-          sa_vl = sa_vl + zlcond2; sa_lv = sa_lv - zlcond2; zqxfg[QL] = zqxfg[QL] + zlcond2;
-        } else {
-          sa_vi = sa_vi + zlcond2; sa_iv = sa_iv - zlcond2; zqxfg[QI] = zqxfg[QI] + zlcond2;
+        if (warm_homo) { sa_lv = sa_lv - zlcond2; zqxfg[QL] = zqxfg[QL] + zlcond2;
+        } else { sa_iv = sa_iv - zlcond2; zqxfg[QI] = zqxfg[QI] + zlcond2;
         }
       }
     }
@@ -457,20 +476,20 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
     // 3.7 growth of ice by vapour deposition, Rotstayn (:1382-1447)
     if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
     else cs.zcldtopdist = cs.zcldtopdist + zdp / (zrho * c.rg);
-    if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
+    if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) { CLOUDSC_BRANCH_COUNT(7);
       const real zvpice = ((c.r2es * e_ice) * c.rv) / c.rd;
       const real zvpliq = zvpice * zfokoop;
-      const real zicenuclei = R(1000.0) * exp((R(12.96) * (zvpliq - zvpice)) / zvpliq - R(0.639));
+      const real zicenuclei = R(1000.0) * cl_exp<real>((R(12.96) * (zvpliq - zvpice)) / zvpliq - R(0.639));
       const real zadd = (c.rlstt * (c.rlstt / (c.rv * ztp1) - R(1.0))) / (R(0.024) * ztp1);
       const real zbdd = ((c.rv * ztp1) * pap_k) / (R(2.21) * zvpice);
-      const real zcvds = ((R(7.8) * pow(zicenuclei / zrho, R(0.666))) * (zvpliq - zvpice)) / ((R(8.87) * (zadd + zbdd)) * zvpice);
+      const real zcvds = ((R(7.8) * cl_pow<real>(zicenuclei / zrho, R(0.666))) * (zvpliq - zvpice)) / ((R(8.87) * (zadd + zbdd)) * zvpice);
       const real zice0 = fmax(zicecld, (zicenuclei * c.riceinit) / zrho);
-      const real zinew = pow((R(0.666) * zcvds) * c.ptsphy + pow(zice0, R(0.666)), R(1.5));
+      const real zinew = cl_pow<real>((R(0.666) * zcvds) * c.ptsphy + cl_pow<real>(zice0, R(0.666)), R(1.5));
       real zdepos = fmax(za * (zinew - zice0), R(0.0));
       zdepos = fmin(zdepos, zqxfg[QL]);
       const real zinfactor = fmin(zicenuclei / R(15000.0), R(1.0));
       zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cs.zcldtopdist / c.rdepliqrefdepth), R(1.0));
-      sa_li = sa_li + zdepos; sa_il = sa_il - zdepos;
+      sa_li = sa_li + zdepos;
       zqxfg[QI] = zqxfg[QI] + zdepos; zqxfg[QL] = zqxfg[QL] - zdepos;
     }
 
@@ -493,7 +512,7 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
 
     // precip cover overlap, MAX-RAN (:1594-1611)
     real zcovpclr, zraincld, zsnowcld;
-    if (zqpretot > zepsec) {
+    if (zqpretot > zepsec) { CLOUDSC_BRANCH_COUNT(8);
       cs.zcovptot = R(1.0) - (R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)) / (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6)));
       cs.zcovptot = fmax(cs.zcovptot, c.rcovpmin);
       zcovpclr = fmax(R(0.0), cs.zcovptot - za);
@@ -506,47 +525,45 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
 
     const bool cold = ztp1 <= c.rtt;
     // 4.3a autoconversion to snow (:1616-1637)
-    if (cold && zicecld > zepsec) {
-      real zzco = c.zzco_snow * exp(c.rsnowlin2 * (ztp1 - c.rtt));
+    if (cold && zicecld > zepsec) { CLOUDSC_BRANCH_COUNT(9);
+      real zzco = c.zzco_snow * cl_exp<real>(c.rsnowlin2 * (ztp1 - c.rtt));
       real zlcrit = c.rlcritsnow;
       if (c.laericeauto) {
         zlcrit = in.picrit_aer;
-        zzco = zzco * pow(c.rnice / in.pnice, R(0.333));
+        zzco = zzco * cl_pow<real>(c.rnice / in.pnice, R(0.333));
       }
       const real r = zicecld / zlcrit;
-      sb_is = sb_is + zzco * (R(1.0) - exp(-(r * r)));
+      sb_is = sb_is + zzco * (R(1.0) - cl_exp<real>(-(r * r)));
     }
     // 4.3b warm rain, Khairoutdinov and Kogan 2000 (:1644-1761)
-    if (zliqcld > zepsec) {
+    if (zliqcld > zepsec) { CLOUDSC_BRANCH_COUNT(10);
       real zrainaut = R(0.0), zrainacc = R(0.0);
-      if (zliqcld > cc.kk_lcrit) {
-        zrainaut = ((((R(1.5) * za) * c.ptsphy) * c.rcl_kkaau) * pow(zliqcld, c.rcl_kkbauq)) * cc.kk_pow;
+      if (zliqcld > cc.kk_lcrit) { CLOUDSC_BRANCH_COUNT(11);
+        zrainaut = ((((R(1.5) * za) * c.ptsphy) * c.rcl_kkaau) * cl_pow<real>(zliqcld, c.rcl_kkbauq)) * cc.kk_pow;
         zrainaut = fmin(zrainaut, zqxfg[QL]);
         if (zrainaut < zepsec) zrainaut = R(0.0);
-        zrainacc = (((R(2.0) * za) * c.ptsphy) * c.rcl_kkaac) * pow(zliqcld * zraincld, c.rcl_kkbac);
+        zrainacc = (((R(2.0) * za) * c.ptsphy) * c.rcl_kkaac) * cl_pow<real>(zliqcld * zraincld, c.rcl_kkbac);
         zrainacc = fmin(zrainacc, zqxfg[QL]);
         if (zrainacc < zepsec) zrainacc = R(0.0);
       }
       if (cold) {
         sa_ls = sa_ls + zrainaut; sa_ls = sa_ls + zrainacc;
-        sa_sl = sa_sl - zrainaut; sa_sl = sa_sl - zrainacc;
       } else {
         sa_lr = sa_lr + zrainaut; sa_lr = sa_lr + zrainacc;
-        sa_rl = sa_rl - zrainaut; sa_rl = sa_rl - zrainacc;
       }
     }
     // riming of snow by cloud water (:1768-1808)
-    if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) {
-      const real zfallcorr = pow(c.rdensref / zrho, R(0.4));
+    if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) { CLOUDSC_BRANCH_COUNT(12);
+      const real zfallcorr = cl_pow<real>(c.rdensref / zrho, R(0.4));
       real zsnowrime = ((((R(0.3) * cs.zcovptot) * c.ptsphy) * c.rcl_const7s) * zfallcorr) *
-                       pow((zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
+                       cl_pow<real>((zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
       zsnowrime = fmin(zsnowrime, R(1.0));
       sb_ls = sb_ls + zsnowrime;
     }
 
     // 4.4a melting of snow and ice (:1817-1859)
     const real zicetot = zqxfg[QI] + zqxfg[QS];
-    if (zicetot > zepsec && ztp1 > c.rtt) {
+    if (zicetot > zepsec && ztp1 > c.rtt) { CLOUDSC_BRANCH_COUNT(13);
       const real zsubsat = fmax(zqsice - zqx[QV], R(0.0));
       const real ztdmtw0 = ztp1 - c.rtt - zsubsat * (ztw1 + ztw2 * (pap_k - ztw3) - ztw4 * (ztp1 - ztw5));
       const real zcons1 = fabs((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)) / c.rtaumel);
@@ -556,19 +573,19 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
           const real zalfa = zqxfg[QI] / zicetot;
           const real zmelt = fmin(zqxfg[QI], zalfa * zmeltmax);
           zqxfg[QI] = zqxfg[QI] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
-          sa_ir = sa_ir + zmelt; sa_ri = sa_ri - zmelt;
+          sa_ir = sa_ir + zmelt;
         }
         {   // snow -> rain
           const real zalfa = zqxfg[QS] / zicetot;
           const real zmelt = fmin(zqxfg[QS], zalfa * zmeltmax);
           zqxfg[QS] = zqxfg[QS] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
-          sa_sr = sa_sr + zmelt; sa_rs = sa_rs - zmelt;
+          sa_sr = sa_sr + zmelt;
         }
       }
     }
 
     // 4.4b freezing of rain (:1864-1908)
-    if (zqx[QR] > zepsec) {
+    if (zqx[QR] > zepsec) { CLOUDSC_BRANCH_COUNT(14);
       if (cold && cs.t_prev > c.rtt) {
         const real tot = fmax(zqx[QS] + zqx[QR], zepsec);
         cs.rainfrac = zqx[QR] / tot;
@@ -576,26 +593,25 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
       if (ztp1 < c.rtt) {
         real zfrzmax;
         if (cs.rainfrac > R(0.8)) {
-          const real zlambda = pow(c.rcl_fac1 / (zrho * zqx[QR]), c.rcl_fac2);
+          const real zlambda = cl_pow<real>(c.rcl_fac1 / (zrho * zqx[QR]), c.rcl_fac2);
           const real ztemp = c.rcl_fzrab * (ztp1 - c.rtt);
-          const real zfrz = ((c.ptsphy * (c.rcl_const5r / zrho)) * (exp(ztemp) - R(1.0))) * pow(zlambda, c.rcl_const6r);
+          const real zfrz = ((c.ptsphy * (c.rcl_const5r / zrho)) * (cl_exp<real>(ztemp) - R(1.0))) * cl_pow<real>(zlambda, c.rcl_const6r);
           zfrzmax = fmax(zfrz, R(0.0));
         } else {
           const real zcons1 = fabs((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))) / c.rtaumel);
           zfrzmax = fmax(((c.rtt - ztp1) * zcons1) * c.zrldcp, R(0.0));
         }
         if (zfrzmax > zepsec) {
-          const real zfrz = fmin(zqx[QR], zfrzmax);
-          sa_rs = sa_rs + zfrz; sa_sr = sa_sr - zfrz;
+          const real zfrz = fmin(zqx[QR], zfrzmax); sa_sr = sa_sr - zfrz;
         }
       }
     }
     // 4.4c freezing of liquid (:1913-1928)
     {
       const real zfrzmax = fmax((c.rthomo - ztp1) * c.zrldcp, R(0.0));
-      if (zfrzmax > zepsec && zqxfg[QL] > zepsec) {
+      if (zfrzmax > zepsec && zqxfg[QL] > zepsec) { CLOUDSC_BRANCH_COUNT(15);
         const real zfrz = fmin(zqxfg[QL], zfrzmax);
-        sa_li = sa_li + zfrz; sa_il = sa_il - zfrz;
+        sa_li = sa_li + zfrz;
       }
     }
 
@@ -605,20 +621,20 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
     {
       const real zzrh = fmin(R(0.8), zzrh0);
       const real zqe = fmax(R(0.0), fmin(zqx[QV], zqsliq));
-      if (zcovpclr > zepsec && zqxfg[QR] > zepsec && zqe < zzrh * zqsliq) {
+      if (zcovpclr > zepsec && zqxfg[QR] > zepsec && zqe < zzrh * zqsliq) { CLOUDSC_BRANCH_COUNT(16);
         const real zpreclr = zqxfg[QR] / cs.zcovptot;
-        const real zfallcorr = pow(c.rdensref / zrho, R(0.4));
+        const real zfallcorr = cl_pow<real>(c.rdensref / zrho, R(0.4));
         const real zesatliq = c.rv_rd * (c.r2es * e_liq);
-        const real zlambda = pow(c.rcl_fac1 / (zrho * zpreclr), c.rcl_fac2);
-        const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * pow(ztp1, R(3.0))) * pap_k;
-        const real zcorr2 = (pow(ztp1 / R(273.0), R(1.5)) * R(393.0)) / (ztp1 + R(120.0));
+        const real zlambda = cl_pow<real>(c.rcl_fac1 / (zrho * zpreclr), c.rcl_fac2);
+        const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * cl_pow<real>(ztp1, R(3.0))) * pap_k;
+        const real zcorr2 = (cl_pow<real>(ztp1 / R(273.0), R(1.5)) * R(393.0)) / (ztp1 + R(120.0));
         const real zsubsat = fmax(zzrh * zqsliq - zqe, R(0.0));
         const real zbeta = ((((R(0.5) / zqsliq) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (zcorr2 / zevap_denom) *
-                           (R(0.78) / pow(zlambda, c.rcl_const4r) + (c.rcl_const2r * sqrt(zrho * zfallcorr)) / (sqrt(zcorr2) * pow(zlambda, c.rcl_const3r)));
+                           (R(0.78) / cl_pow<real>(zlambda, c.rcl_const4r) + (c.rcl_const2r * sqrt(zrho * zfallcorr)) / (sqrt(zcorr2) * cl_pow<real>(zlambda, c.rcl_const3r)));
         const real zdenom = R(1.0) + zbeta * c.ptsphy;
         const real zdpevap = (((zcovpclr * zbeta) * c.ptsphy) * zsubsat) / zdenom;
         const real zevap = fmin(zdpevap, zqxfg[QR]);
-        sa_rv = sa_rv + zevap; sa_vr = sa_vr - zevap;
+        sa_rv = sa_rv + zevap;
         cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), ((cs.zcovptot - za) * zevap) / zqxfg[QR]));
         zqxfg[QR] = zqxfg[QR] - zevap;
       }
@@ -628,23 +644,23 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
       const real zzrh = zzrh0;
       real zqe = (zqx[QV] - za * zqsice) / fmax(zepsec, R(1.0) - za);
       zqe = fmax(R(0.0), fmin(zqe, zqsice));
-      if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) {
+      if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) { CLOUDSC_BRANCH_COUNT(17);
         const real x = cs.zcovptot * zdtgdp;
         const real zpreclr = (zqxfg[QS] * zcovpclr) / copysign(fmax(fabs(x), zepsilon), x);
         const real zbeta1 = ((sqrt(pap_k / cc.paph_sfc) / c.rvrfactor) * zpreclr) / fmax(zcovpclr, zepsec);
-        const real zbeta = c.rg_rpecons * pow(zbeta1, R(0.5777));
+        const real zbeta = c.rg_rpecons * cl_pow<real>(zbeta1, R(0.5777));
         const real zdenom = R(1.0) + (zbeta * c.ptsphy) * zcorqsice;
         const real zdpr = ((((zcovpclr * zbeta) * (zqsice - zqe)) / zdenom) * zdp) * c.zrg_r;
         const real zdpevap = zdpr * zdtgdp;
         const real zevap = fmin(zdpevap, zqxfg[QS]);
-        sa_sv = sa_sv + zevap; sa_vs = sa_vs - zevap;
+        sa_sv = sa_sv + zevap;
         cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), ((cs.zcovptot - za) * zevap) / zqxfg[QS]));
         zqxfg[QS] = zqxfg[QS] - zevap;
       }
     }
     // evaporate small precipitation amounts (:2144-2158)
-    if (zqxfg[QR] < c.rlmin) { sa_rv = sa_rv + zqxfg[QR]; sa_vr = sa_vr - zqxfg[QR]; }
-    if (zqxfg[QS] < c.rlmin) { sa_sv = sa_sv + zqxfg[QS]; sa_vs = sa_vs - zqxfg[QS]; }
+    if (zqxfg[QR] < c.rlmin) { sa_rv = sa_rv + zqxfg[QR]; }
+    if (zqxfg[QS] < c.rlmin) { sa_sv = sa_sv + zqxfg[QS]; }
 
     // 5.1 cloud cover (:2168-2180)
     real zanew = (za + zsolac) / (R(1.0) + zsolab);
@@ -662,42 +678,42 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
     {
       real z = R(0.0), psum, zrat;
       // m = ql: zsolqa[n][ql] = {ll, il, rl, sl, vl}
-      psum = R(0.0) + sa_ll; psum = psum + sa_il; psum = psum + sa_rl; psum = psum + sa_sl; psum = psum + sa_vl;
+      psum = R(0.0) + sa_ll; psum = psum + (-sa_li); psum = psum + (-sa_lr); psum = psum + (-sa_ls); psum = psum + (-sa_lv);
       { const real zmm = fmax(zqx[QL], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
       if (sa_ll < R(0.0)) { sa_ll = sa_ll * zrat; sa_ll = sa_ll * zrat; }
-      if (sa_il < R(0.0)) { sa_il = sa_il * zrat; sa_li = sa_li * zrat; }
-      if (sa_rl < R(0.0)) { sa_rl = sa_rl * zrat; sa_lr = sa_lr * zrat; }
-      if (sa_sl < R(0.0)) { sa_sl = sa_sl * zrat; sa_ls = sa_ls * zrat; }
-      if (sa_vl < R(0.0)) { sa_vl = sa_vl * zrat; sa_lv = sa_lv * zrat; }
+      if (-sa_li < R(0.0)) sa_li = sa_li * zrat;
+      if (-sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
+      if (-sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
+      if (-sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
       // m = qi: {li, ii, ri, si(0), vi}
-      psum = R(0.0) + sa_li; psum = psum + sa_ii; psum = psum + sa_ri; psum = psum + z; psum = psum + sa_vi;
+      psum = R(0.0) + sa_li; psum = psum + sa_ii; psum = psum + (-sa_ir); psum = psum + z; psum = psum + (-sa_iv);
       { const real zmm = fmax(zqx[QI], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
-      if (sa_li < R(0.0)) { sa_li = sa_li * zrat; sa_il = sa_il * zrat; }
+      if (sa_li < R(0.0)) sa_li = sa_li * zrat;
       if (sa_ii < R(0.0)) { sa_ii = sa_ii * zrat; sa_ii = sa_ii * zrat; }
-      if (sa_ri < R(0.0)) { sa_ri = sa_ri * zrat; sa_ir = sa_ir * zrat; }
-      if (sa_vi < R(0.0)) { sa_vi = sa_vi * zrat; sa_iv = sa_iv * zrat; }
+      if (-sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
+      if (-sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
       // m = qr: {lr, ir, rr, sr, vr}
-      psum = R(0.0) + sa_lr; psum = psum + sa_ir; psum = psum + sa_rr; psum = psum + sa_sr; psum = psum + sa_vr;
+      psum = R(0.0) + sa_lr; psum = psum + sa_ir; psum = psum + sa_rr; psum = psum + sa_sr; psum = psum + (-sa_rv);
       { const real zmm = fmax(zqx[QR], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
-      if (sa_lr < R(0.0)) { sa_lr = sa_lr * zrat; sa_rl = sa_rl * zrat; }
-      if (sa_ir < R(0.0)) { sa_ir = sa_ir * zrat; sa_ri = sa_ri * zrat; }
+      if (sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
+      if (sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
       if (sa_rr < R(0.0)) { sa_rr = sa_rr * zrat; sa_rr = sa_rr * zrat; }
-      if (sa_sr < R(0.0)) { sa_sr = sa_sr * zrat; sa_rs = sa_rs * zrat; }
-      if (sa_vr < R(0.0)) { sa_vr = sa_vr * zrat; sa_rv = sa_rv * zrat; }
+      if (sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
+      if (-sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
       // m = qs: {ls, is(0), rs, ss, vs}
-      psum = R(0.0) + sa_ls; psum = psum + z; psum = psum + sa_rs; psum = psum + sa_ss; psum = psum + sa_vs;
+      psum = R(0.0) + sa_ls; psum = psum + z; psum = psum + (-sa_sr); psum = psum + sa_ss; psum = psum + (-sa_sv);
       { const real zmm = fmax(zqx[QS], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
-      if (sa_ls < R(0.0)) { sa_ls = sa_ls * zrat; sa_sl = sa_sl * zrat; }
-      if (sa_rs < R(0.0)) { sa_rs = sa_rs * zrat; sa_sr = sa_sr * zrat; }
+      if (sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
+      if (-sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
       if (sa_ss < R(0.0)) { sa_ss = sa_ss * zrat; sa_ss = sa_ss * zrat; }
-      if (sa_vs < R(0.0)) { sa_vs = sa_vs * zrat; sa_sv = sa_sv * zrat; }
+      if (-sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
       // m = qv: {lv, iv, rv, sv, vv(0)}
       psum = R(0.0) + sa_lv; psum = psum + sa_iv; psum = psum + sa_rv; psum = psum + sa_sv; psum = psum + z;
       { const real zmm = fmax(zqx[QV], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
-      if (sa_lv < R(0.0)) { sa_lv = sa_lv * zrat; sa_vl = sa_vl * zrat; }
-      if (sa_iv < R(0.0)) { sa_iv = sa_iv * zrat; sa_vi = sa_vi * zrat; }
-      if (sa_rv < R(0.0)) { sa_rv = sa_rv * zrat; sa_vr = sa_vr * zrat; }
-      if (sa_sv < R(0.0)) { sa_sv = sa_sv * zrat; sa_vs = sa_vs * zrat; }
+      if (sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
+      if (sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
+      if (sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
+      if (sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
     }
 
     // 5.2.2 implicit solver (:2294-2397).  With the zsolqb sparsity above,
@@ -710,13 +726,13 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
     {
       // RHS: zqxn[m] = zqx[m] + sum_n zsolqa[n][m], n ascending from 0.0
       real ex;
-      ex = R(0.0) + sa_ll; ex = ex + sa_il; ex = ex + sa_rl; ex = ex + sa_sl; ex = ex + sa_vl;
+      ex = R(0.0) + sa_ll; ex = ex + (-sa_li); ex = ex + (-sa_lr); ex = ex + (-sa_ls); ex = ex + (-sa_lv);
       real qn_l = zqx[QL] + ex;
-      ex = R(0.0) + sa_li; ex = ex + sa_ii; ex = ex + sa_ri; ex = ex + R(0.0); ex = ex + sa_vi;
+      ex = R(0.0) + sa_li; ex = ex + sa_ii; ex = ex + (-sa_ir); ex = ex + R(0.0); ex = ex + (-sa_iv);
       real qn_i = zqx[QI] + ex;
-      ex = R(0.0) + sa_lr; ex = ex + sa_ir; ex = ex + sa_rr; ex = ex + sa_sr; ex = ex + sa_vr;
+      ex = R(0.0) + sa_lr; ex = ex + sa_ir; ex = ex + sa_rr; ex = ex + sa_sr; ex = ex + (-sa_rv);
       real qn_r = zqx[QR] + ex;
-      ex = R(0.0) + sa_ls; ex = ex + R(0.0); ex = ex + sa_rs; ex = ex + sa_ss; ex = ex + sa_vs;
+      ex = R(0.0) + sa_ls; ex = ex + R(0.0); ex = ex + (-sa_sr); ex = ex + sa_ss; ex = ex + (-sa_sv);
       real qn_s = zqx[QS] + ex;
       ex = R(0.0) + sa_lv; ex = ex + sa_iv; ex = ex + sa_rv; ex = ex + sa_sv; ex = ex + R(0.0);
       real qn_v = zqx[QV] + ex;
@@ -774,8 +790,8 @@ __device__ __forceinline__ void physics_level(const DevParams<real>& c, const in
 }
 
 // ===== 8. flux diagnostics of one level (cloudsc_c.c:2521-2582), written at half level k+1 =====
-template <typename real>
-__device__ __forceinline__ void flux_level(const DevParams<real>& c, const KArgs<real>& A, size_t h, unsigned lo,
+template <typename real, typename P>
+__device__ __forceinline__ void flux_level(const P& c, const KArgs<real>& A, size_t h, unsigned lo,
                                            const LevelIn<real>& in, const LevelState<real>& ls,
                                            const PhysOut<real>& po, real paph_k, real paph_n,
                                            CarryState<real>& cs) {
@@ -806,8 +822,8 @@ __device__ __forceinline__ void flux_level(const DevParams<real>& c, const KArgs
 }
 
 // level-0 half-level outputs (cloudsc_c.c:2523-2543, 2578-2579)
-template <typename real>
-__device__ __forceinline__ void flux_top(const DevParams<real>& c, const KArgs<real>& A, size_t h0, unsigned lo) {
+template <typename real, typename P>
+__device__ __forceinline__ void flux_top(const P& c, const KArgs<real>& A, size_t h0, unsigned lo) {
   stg(A.pfsqlf, h0, lo, R(0.0)); stg(A.pfsqif, h0, lo, R(0.0)); stg(A.pfsqrf, h0, lo, R(0.0));
   stg(A.pfsqsf, h0, lo, R(0.0)); stg(A.pfcqlng, h0, lo, R(0.0)); stg(A.pfcqnng, h0, lo, R(0.0));
   stg(A.pfcqrng, h0, lo, R(0.0)); stg(A.pfcqsng, h0, lo, R(0.0));
@@ -817,8 +833,8 @@ __device__ __forceinline__ void flux_top(const DevParams<real>& c, const KArgs<r
   stg(A.pfhpsl, h0, lo, -c.rlvtt * plsl); stg(A.pfhpsn, h0, lo, -c.rlstt * plsn);
 }
 
-template <typename real>
-__device__ __forceinline__ ColConst<real> column_constants(const DevParams<real>& c, const KArgs<real>& A,
+template <typename real, typename P>
+__device__ __forceinline__ ColConst<real> column_constants(const P& c, const KArgs<real>& A,
                                                            size_t u1, size_t uh, unsigned lo) {
   ColConst<real> cc;
   const real plsm = ldg(A.plsm, u1, lo);
@@ -827,7 +843,7 @@ __device__ __forceinline__ ColConst<real> column_constants(const DevParams<real>
   const bool land = plsm > R(0.5);
   cc.kk_const = land ? c.rcl_kk_cloud_num_land : c.rcl_kk_cloud_num_sea;
   cc.kk_lcrit = land ? c.rclcrit_land : c.rclcrit_sea;
-  cc.kk_pow = pow(cc.kk_const, c.rcl_kkbaun);   // loop-invariant factor of the KK autoconversion (:1721)
+  cc.kk_pow = cl_pow<real>(cc.kk_const, c.rcl_kkbaun);   // loop-invariant factor of the KK autoconversion (:1721)
   return cc;
 }
 
@@ -840,7 +856,7 @@ __device__ __forceinline__ void store_level(const KArgs<real>& A, size_t u2, siz
   stg(A.tlq, i, lo, ls.qtend);
   stg(A.tla, i, lo, po.atend);
   stg(A.pcovptot, i, lo, po.zcovptot_out);
-  if (physics && k < klev - 1) stg(A.plude, i, lo, po.plude_k);   // INOUT: untouched elsewhere
+  stg(A.plude, i, lo, po.plude_k);   // INOUT: rewritten unchanged where not rescaled (no branch on a store)
 #pragma unroll
   for (int m = 0; m < 4; m++) stg(A.tlcld, u3 + ((size_t)m * klev + k) * nproma, lo, po.ctend[m]);
   stg(A.tlcld, u3 + ((size_t)4 * klev + k) * nproma, lo, R(0.0));
@@ -859,62 +875,66 @@ __device__ __forceinline__ void init_carry(CarryState<real>& cs) {
 // `ka` points at the kernel's KArgs in the kernarg segment and `cpar` at the
 // __constant__ parameter block, both in the constant address space; they are
 // re-laundered every level so that scalar loads are issued where needed.
-template <typename real>
-__device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar) {
+// PF selects the load schedule: 1 = level k+1 prefetched into registers while
+// level k computes; 0 = loads issued at the top of their own level.
+//
+// kcache_levels runs levels [lev0, lev1) of block b for one (active) lane with
+// the carried state `cs`; the plain kernel runs [0, klev) in one go, the
+// persistent kernel (below) runs a column in level segments.
+template <typename real, int PF, bool AER>
+__device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar, int b,
+                                              unsigned lo, int lev0, int lev1, CarryState<real>& cs) {
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int nproma = A0.nproma, klev = A0.klev;
-  const int b = blockIdx.x, jl = threadIdx.x;
-  if (jl >= nproma || b * nproma + jl >= A0.ngptot) return;
-  const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);       // lane byte offset
   const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
   const size_t u2 = (size_t)b * klev * nproma;                     // [nblocks][klev][nproma]
   const size_t uh = (size_t)b * (klev + 1) * nproma;               // [nblocks][klev+1][nproma]
   const size_t u3 = (size_t)b * 5 * klev * nproma;                 // [nblocks][5][klev][nproma]
 
   ColConst<real> cc;
-  CarryState<real> cs;
   Neighbors<real> nb;
   LevelIn<real> cur, nxt;
   int ncldtop0;
   {
-    const DevParams<real>& c = *(const DevParams<real>*)cpar;
+    CLOUDSC_PARAMS_HERE;
     const KArgs<real>& A = A0;
     ncldtop0 = c.ncldtop - 1;
     cc = column_constants(c, A, u1, uh, lo);
-    init_carry(cs);
-    flux_top(c, A, uh, lo);
-    nb.paph_k = ldg(A.paph, uh, lo);
-    nb.paph_n = ldg(A.paph, uh + nproma, lo);
-    nb.pmfu_k = ldg(A.pmfu, u2, lo); nb.pmfd_k = ldg(A.pmfd, u2, lo);
-    nb.pmfu_n = ldg(A.pmfu, u2 + nproma, lo); nb.pmfd_n = ldg(A.pmfd, u2 + nproma, lo);
-    nb.plu_n = ldg(A.plu, u2 + nproma, lo);
-    load_level(cur, A, c, u2, u3, 0, klev, nproma, lo, ncldtop0 <= 0);
+    const int l1 = lev0 + 1 < klev ? lev0 + 1 : klev - 1;
+    nb.paph_k = ldg(A.paph, uh + (size_t)lev0 * nproma, lo);
+    nb.paph_n = ldg(A.paph, uh + (size_t)(lev0 + 1) * nproma, lo);
+    nb.pmfu_k = ldg(A.pmfu, u2 + (size_t)lev0 * nproma, lo);
+    nb.pmfd_k = ldg(A.pmfd, u2 + (size_t)lev0 * nproma, lo);
+    nb.pmfu_n = ldg(A.pmfu, u2 + (size_t)l1 * nproma, lo);
+    nb.pmfd_n = ldg(A.pmfd, u2 + (size_t)l1 * nproma, lo);
+    nb.plu_n = ldg(A.plu, u2 + (size_t)l1 * nproma, lo);
+    if (PF) load_level<real, AER>(cur, A, u2, u3, lev0, klev, nproma, lo);
   }
 
-  for (int kloop = 0; kloop < klev; kloop++) {
+  for (int kloop = lev0; kloop < lev1; kloop++) {
     // the level index is laundered too, so no per-field induction pointers are formed
     int k = kloop;
     asm volatile("" : "+s"(k));
     const bool physics = k >= ncldtop0;
     // ---- issue the loads of the next levels (software pipelining) ----
-    real paph_nn = R(0.0), pmfu_nn = R(0.0), pmfd_nn = R(0.0), plu_nn = R(0.0);
+    real paph_nn, pmfu_nn, pmfd_nn, plu_nn;
     {
       const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
-      const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar);
-      if (k + 1 < klev) {
-        load_level(nxt, A, c, u2, u3, k + 1, klev, nproma, lo, k + 1 >= ncldtop0);
-        paph_nn = ldg(A.paph, uh + (size_t)(k + 2) * nproma, lo);
-        if (k + 2 < klev) {
-          const size_t i2 = u2 + (size_t)(k + 2) * nproma;
-          pmfu_nn = ldg(A.pmfu, i2, lo); pmfd_nn = ldg(A.pmfd, i2, lo); plu_nn = ldg(A.plu, i2, lo);
-        }
-      }
+      // indices clamped instead of branched: the last levels re-read valid data
+      const int k1 = k + 1 < klev ? k + 1 : klev - 1;
+      const int k2 = k + 2 < klev ? k + 2 : klev - 1;
+      const int kh2 = k + 2 < klev + 1 ? k + 2 : klev;
+      if (!PF) load_level<real, AER>(cur, A, u2, u3, k, klev, nproma, lo);
+      if (PF) load_level<real, AER>(nxt, A, u2, u3, k1, klev, nproma, lo);
+      paph_nn = ldg(A.paph, uh + (size_t)kh2 * nproma, lo);
+      const size_t i2 = u2 + (size_t)k2 * nproma;
+      pmfu_nn = ldg(A.pmfu, i2, lo); pmfd_nn = ldg(A.pmfd, i2, lo); plu_nn = ldg(A.plu, i2, lo);
     }
 
     LevelState<real> ls;
     PhysOut<real> po;
     {
-      const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar);
+      CLOUDSC_PARAMS_HERE;
       init_level(c, cur, ls);
 #pragma unroll
       for (int m = 0; m < 4; m++) { po.zqxn[m] = R(0.0); po.ctend[m] = R(0.0); }
@@ -925,7 +945,7 @@ __device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<D
     }
     {
       const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
-      const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar);
+      CLOUDSC_PARAMS_HERE;
       store_level(A, u2, u3, k, klev, nproma, lo, physics, ls, po);
       flux_level(c, A, uh + (size_t)(k + 1) * nproma, lo, cur, ls, po, nb.paph_k, nb.paph_n, cs);
     }
@@ -935,11 +955,139 @@ __device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<D
     nb.paph_k = nb.paph_n; nb.paph_n = paph_nn;
     nb.pmfu_k = nb.pmfu_n; nb.pmfd_k = nb.pmfd_n;
     nb.pmfu_n = pmfu_nn; nb.pmfd_n = pmfd_nn; nb.plu_n = plu_nn;
-    cur = nxt;
+    if (PF) cur = nxt;
   }
+}
+
+template <typename real, int PF, bool AER>
+__device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar) {
+  const KArgs<real>& A = *(const KArgs<real>*)ka;
+  const int b = blockIdx.x, jl = threadIdx.x;
+  if (jl >= A.nproma || b * A.nproma + jl >= A.ngptot) return;
+  const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
+  CarryState<real> cs;
+  init_carry(cs);
   {
-    const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
-    stg(A.prainfrac, u1, lo, cs.rainfrac);
+    CLOUDSC_PARAMS_HERE;
+    flux_top(c, A, (size_t)b * (A.klev + 1) * A.nproma, lo);
+  }
+  kcache_levels<real, PF, AER>(ka, cpar, b, lo, 0, A.klev, cs);
+  stg(((const KArgs<real>*)launder_uniform(ka))->prainfrac, (size_t)b * A.nproma, lo, cs.rainfrac);
+}
+
+// ===================== persistent (work-queue) SCC-k-caching =====================
+// Each column's level loop is cut into NSEG segments; an item is (segment s,
+// block b), dequeued in order s-major from an atomic counter.  Segment s of
+// block b waits for segment s-1 of b (flag[b] >= s) and resumes from the carried
+// state it left in HBM ([nblocks][kCarryN][nproma], 19 values per column), so
+// the result is bit-identical to the one-shot kernel.  Dequeue order guarantees
+// progress: an item's predecessor was dequeued earlier by a running workgroup.
+// The point: 2560 waves on 2048 wave slots leave the second round 75 % idle;
+// with NSEG segments the tail shrinks to a fraction of a segment.
+constexpr int kCarryN = 19;
+constexpr int kMaxSeg = 8;
+
+#ifdef CLOUDSC_KSEG_TRACE
+constexpr int kTraceMax = 1 << 16;
+__device__ unsigned long long g_kseg_trace[4 * kTraceMax];
+#endif
+
+template <typename real>
+struct PersistArgs {
+  unsigned* counter;      // dequeue counter (zeroed per launch)
+  unsigned* flags;        // [nblocks] segments completed (zeroed per launch)
+  unsigned* err;          // spin-limit violations (zeroed per launch)
+  real* state;            // [nblocks][kCarryN][nproma]
+  int nseg, nitems, nblocks;
+  int lev[kMaxSeg + 1];
+};
+
+// write-through (sc1) store of a handed-off value: an agent-scope relaxed atomic
+// store lowers to global_store sc1, so the hand-off needs no L2 write-back
+// (release fence) on the producer side (cdna_hip_programming.md G16, R1)
+__device__ __forceinline__ void stg_sc1(double* ubase, size_t uidx, unsigned lane_bytes, double v) {
+  __hip_atomic_store((unsigned long long*)((char*)(ubase + uidx) + lane_bytes), __double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stg_sc1(float* ubase, size_t uidx, unsigned lane_bytes, float v) {
+  __hip_atomic_store((unsigned*)((char*)(ubase + uidx) + lane_bytes), __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename real>
+__device__ __forceinline__ void carry_io(real* st, size_t u, size_t plane, unsigned lo, CarryState<real>& cs,
+                                         bool save) {
+  real* f[kCarryN] = {&cs.t_prev, &cs.a_prev, &cs.pap_prev, &cs.zanewm1, &cs.zcovptot, &cs.zcovpmax,
+                      &cs.zcldtopdist, &cs.rainfrac, &cs.qxnm1_l, &cs.qxnm1_i, &cs.pfx_i, &cs.pfx_r, &cs.pfx_s,
+                      &cs.fl_lf, &cs.fl_if, &cs.fl_lng, &cs.fl_nng, &cs.fl_ltur, &cs.fl_itur};
+#pragma unroll
+  for (int q = 0; q < kCarryN; q++) {
+    if (save) stg_sc1(st, u + (size_t)q * plane, lo, *f[q]);
+    else *f[q] = ldg((const real*)st, u + (size_t)q * plane, lo);
+  }
+}
+
+template <typename real, int PF, bool AER>
+__device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar,
+                                                               const PersistArgs<real>& P) {
+  __shared__ int s_item;
+  const KArgs<real>& A = *(const KArgs<real>*)ka;
+  const int nproma = A.nproma, jl = threadIdx.x;
+  const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
+  for (;;) {
+    if (jl == 0) s_item = (int)__hip_atomic_fetch_add(P.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int item = s_item;
+    __syncthreads();                                   // s_item is rewritten next iteration
+    if (item >= P.nitems) break;
+    const int seg = item / P.nblocks, b = item - seg * P.nblocks;
+#ifdef CLOUDSC_KSEG_TRACE
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    const bool active = jl < nproma && b * nproma + jl < A.ngptot;
+    const size_t ust = (size_t)b * kCarryN * nproma;
+    CarryState<real> cs;
+    if (seg == 0) {
+      init_carry(cs);
+      if (active) {
+        CLOUDSC_PARAMS_HERE;
+        flux_top(c, A, (size_t)b * (A.klev + 1) * nproma, lo);
+      }
+    } else {
+      // consumer: one relaxed poll, one agent acquire, wait, barrier, plain loads
+      if (jl == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(P.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)seg) {
+          __builtin_amdgcn_s_sleep(4);
+          if (++spins > (1u << 24)) { atomicAdd(P.err, 1u); break; }   // bounded: never hang
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, false);
+    }
+    if (active) kcache_levels<real, PF, AER>(ka, cpar, b, lo, P.lev[seg], P.lev[seg + 1], cs);
+    if (seg + 1 < P.nseg) {
+      // producer (G16 R1): sc1 payload stores, every wave drains, barrier, one
+      // lane stores the flag with an agent atomic; no L2 write-back needed
+      if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, true);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (jl == 0)
+        __hip_atomic_store(P.flags + b, (unsigned)(seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (active) {
+      stg(((const KArgs<real>*)launder_uniform(ka))->prainfrac, (size_t)b * nproma, lo, cs.rainfrac);
+    }
+#ifdef CLOUDSC_KSEG_TRACE
+    if (jl == 0 && item < kTraceMax) {   // diagnostic build only: schedule of every item
+      g_kseg_trace[4 * item + 0] = t_start;
+      g_kseg_trace[4 * item + 1] = __builtin_amdgcn_s_memrealtime();
+      g_kseg_trace[4 * item + 2] = blockIdx.x;
+      g_kseg_trace[4 * item + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) * 65536ull +
+                                   __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+    }
+#endif
   }
 }
 

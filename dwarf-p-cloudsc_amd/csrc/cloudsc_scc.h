@@ -67,7 +67,7 @@ __device__ __forceinline__ void scc_get_ls(const real* base, size_t idx, size_t 
   for (int m = 0; m < 4; m++) s.zlneg[m] = ldg(base, idx + (15 + m) * plane, lo);
 }
 
-template <typename real>
+template <typename real, bool AER>
 __device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const SccScratch<real> S,
                                                  cptr<DevParams<real>> cpar) {
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
@@ -91,7 +91,7 @@ __device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const Scc
   // ---- sweep 1: section 1 for every level ----
   for (int k = 0; k < klev; k++) {
     LevelIn<real> in;
-    load_level(in, SCC_A, SCC_C, u2, u3, k, klev, nproma, lo, false);
+    load_level<real, AER>(in, SCC_A, u2, u3, k, klev, nproma, lo);
     LevelState<real> ls;
     init_level(SCC_C, in, ls);
     scc_put_ls(S.ls, ulsb + (size_t)k * nproma, plane, lo, ls);
@@ -107,7 +107,7 @@ __device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const Scc
     const bool physics = k >= ncldtop0;
     const KArgs<real>& A = SCC_A;
     LevelIn<real> in;
-    load_level(in, A, SCC_C, u2, u3, k, klev, nproma, lo, physics);
+    load_level<real, AER>(in, A, u2, u3, k, klev, nproma, lo);
     LevelState<real> ls;
     scc_get_ls((const real*)S.ls, ulsb + (size_t)k * nproma, plane, lo, ls);
     Neighbors<real> nb;

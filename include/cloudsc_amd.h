@@ -59,6 +59,8 @@ extern "C" {
 /* kernel variant selector */
 #define CLOUDSC_VARIANT_SCC    1   /* SCC baseline: level phases as separate sweeps, temporaries in HBM scratch */
 #define CLOUDSC_VARIANT_KCACHE 2   /* SCC-k-caching: one fused level loop, carried state in registers       */
+#define CLOUDSC_VARIANT_KSEG   3   /* SCC-k-caching, persistent work queue over (level segment, block)      */
+                                   /* items; carried state handed between segments through HBM scratch   */
 
 /* error codes */
 #define CLOUDSC_OK            0
@@ -136,13 +138,15 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t *params);
 /* Enqueue one CLOUDSC step over ngptot columns on `stream` (a hipStream_t, or
  * NULL for the default stream) of `device`.  Asynchronous; errors in the launch
  * configuration are returned, asynchronous faults surface at the caller's sync.
- * SCC needs a workspace: pass scratch of cloudsc_gpu_scratch_bytes() bytes (or
- * NULL for KCACHE). */
+ * SCC and KSEG need a workspace: pass scratch of cloudsc_gpu_scratch_bytes()
+ * bytes (NULL is fine for KCACHE).  The KSEG workspace holds a dequeue counter
+ * and per-block flags that are re-zeroed on `stream` before every launch, so one
+ * workspace must not be shared by launches in flight on different streams. */
 int cloudsc_gpu_run(int device, void *stream, int precision, int variant,
                     int ngptot, int nproma, int klev,
                     const cloudsc_fields_t *device_fields, void *scratch);
 
-/* Bytes of device scratch the SCC variant needs for (ngptot, nproma, klev, precision). */
+/* Bytes of device scratch a variant needs for (ngptot, nproma, klev, precision); 0 for KCACHE. */
 long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev);
 
 /* Human-readable message for an error code; last HIP error string of this thread. */

@@ -225,3 +225,65 @@ def test_low_level_run_entry(lib, ds):
     ref = run_gpu(ds, 256, 128)
     for _, k in ca.VALIDATED:
         assert np.array_equal(out[k], ref[k]), k
+
+
+# ---- persistent segmented k-caching (KSEG): must be bit-identical to KCACHE ----
+@pytest.fixture
+def kseg_env():
+    import os
+    saved = {k: os.environ.get(k) for k in ("CLOUDSC_KSEG_NSEG", "CLOUDSC_KSEG_GRID")}
+
+    def set_env(nseg=None, grid=None):
+        for k, v in (("CLOUDSC_KSEG_NSEG", nseg), ("CLOUDSC_KSEG_GRID", grid)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+    yield set_env
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+@pytest.mark.parametrize("nseg,grid", [(1, None), (2, None), (4, None), (8, None), (4, 3), (8, 1), (3, 5)])
+def test_kseg_equals_kcache_bitwise(lib, ds, kseg_env, nseg, grid):
+    # grid 1 / 3 / 5: few workgroups, so most segments wait on a predecessor
+    # that another (or the same) workgroup finished earlier
+    a = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KCACHE)
+    kseg_env(nseg, grid)
+    b = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KSEG)
+    for _, k in ca.VALIDATED:
+        assert np.array_equal(a[k], b[k]), (nseg, grid, k)
+
+
+@pytest.mark.parametrize("name", ["W", "M"])
+def test_kseg_scenarios(lib, scenarios, kseg_env, name):
+    s = scenarios[name]
+    kseg_env(4, None)
+    out = run_gpu(s, 100, 128, variant=ca.VARIANT_KSEG)
+    assert_close(field_report(out, s.reference), RELL1_FP64, MAXREL_FP64, "kseg scenario %s" % name)
+
+
+def test_kseg_fp32_equals_kcache_bitwise(lib, ds, kseg_env):
+    a = run_gpu(ds, 1000, 128, precision=ca.FP32, variant=ca.VARIANT_KCACHE)
+    kseg_env(4, 7)
+    b = run_gpu(ds, 1000, 128, precision=ca.FP32, variant=ca.VARIANT_KSEG)
+    for _, k in ca.VALIDATED:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_kseg_full_size(lib, ds, kseg_env):
+    """BASELINE size with the default segmentation and grid: bit-identical to
+    KCACHE on every validated field, repeated launches reuse the workspace."""
+    kseg_env(None, None)
+    g = ca.GpuState(ds, 163840, 128)
+    try:
+        g.run(ca.VARIANT_KCACHE, 1)
+        a = {k: g.download(k) for _, k in ca.VALIDATED}
+        g.run(ca.VARIANT_KSEG, 3)
+        for _, k in ca.VALIDATED:
+            assert np.array_equal(a[k], g.download(k)), k
+    finally:
+        g.close()
