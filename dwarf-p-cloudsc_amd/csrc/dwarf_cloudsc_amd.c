@@ -1,0 +1,370 @@
+/*
+ * dwarf_cloudsc_amd.c -- the dwarf host driver for MI355X:
+ *
+ *   dwarf-cloudsc-amd <nthreads> <ngptot> <nproma> [options]
+ *
+ * Same CLI, flow and stdout format as the reference C dwarf
+ * (src/cloudsc_c/dwarf_cloudsc.c:17-50, cloudsc_driver.c:33-263): load the
+ * KLON-column state (load_state.c), expand it to NGPTOT columns in NPROMA
+ * blocks, run CLOUDSC, print the timing table, validate the 21 output fields
+ * against the reference (cloudsc_validate.c:186-216).  Differences, all on
+ * purpose:
+ *   - the kernel runs on the GPU(s) through libcloudsc_amd.so (include/
+ *     cloudsc_amd.h); expansion and the validation statistics run on the
+ *     device against the KLON-column reference with the g % klon map, so no
+ *     NGPTOT-sized host arrays exist;
+ *   - HDF5 files are opened read-only (load_state.c:60,499,746 open RDWR);
+ *     without input.h5 the raw dataset (tests/golden/cloudsc100) is read;
+ *   - validation uses fabs like the Fortran ERROR_PRINT (validate_mod.F90:
+ *     263-296), not the C validator's integer abs (cloudsc_validate.c:74);
+ *   - the TOTAL line's col/s is NGPTOT/time (cloudsc_driver.c:261 prints the
+ *     last thread's value);
+ *   - exit status 1 if any field's relative L1 error exceeds the gate
+ *     (--tol, default 1e-12 in fp64; fp32 is reported without a gate unless
+ *     --tol is given);
+ *   - --gpus N shards the columns over N devices (block-aligned contiguous
+ *     ranges of the GLOBAL column index, one host thread + stream per device,
+ *     no collective); statistics are combined on the host like the
+ *     MPI_Reduce of validate_mod.F90:53-55.
+ *
+ * nthreads is accepted and printed as NUMOMP for compatibility; the host
+ * threads are one per device.
+ */
+#define _GNU_SOURCE
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "cloudsc_amd.h"
+#include "cloudsc_io.h"
+
+#define ZHPM 12482329.0   /* HPM flop count for 100 columns (cloudsc_driver.c:101) */
+
+typedef struct {
+  int numomp, ngptot, nproma, ngpus, precision, variant, reps, warmup;
+  double tol;
+  int tol_given;
+  const char *input_h5, *reference_h5, *data_dir, *write_h5_dir;
+} options_t;
+
+typedef struct {
+  int device, ngptot, nproma, precision, variant, reps, warmup;
+  long long col_offset;
+  const cloudsc_template_t *tmpl;
+  const cloudsc_params_t *params;
+  const cloudsc_reference_t *ref;
+  pthread_barrier_t *barrier;
+  /* results */
+  int rc;
+  double t_start, t_end;          /* seconds, CLOCK_MONOTONIC */
+  float *kernel_ms;
+  cloudsc_stats_t stats[CLOUDSC_NVALID];
+} shard_t;
+
+static double now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static void usage(const char *prog) {
+  fprintf(stderr,
+          "usage: %s [<nthreads> <ngptot> <nproma>] [options]\n"
+          "  --gpus N              shard the columns over N devices (default 1)\n"
+          "  --precision fp64|fp32 (default fp64)\n"
+          "  --variant kseg|kcache|scc (default kseg)\n"
+          "  --reps R              timed steps (default 1)\n"
+          "  --warmup W            untimed steps before the timed ones (default 1)\n"
+          "  --input FILE          input HDF5 file (default ./input.h5 when present)\n"
+          "  --reference FILE      reference HDF5 file (default ./reference.h5 when present)\n"
+          "  --data DIR            raw dataset directory (default $CLOUDSC_DATA or the\n"
+          "                        repository's tests/golden/cloudsc100)\n"
+          "  --tol X               relative L1 gate per field (default 1e-12 for fp64)\n"
+          "  --write-h5 DIR        write DIR/input.h5 and DIR/reference.h5 of the loaded\n"
+          "                        dataset and exit\n",
+          prog);
+}
+
+static int parse(int argc, char **argv, options_t *o) {
+  memset(o, 0, sizeof(*o));
+  o->numomp = 1; o->ngptot = 100; o->nproma = 4;     /* dwarf_cloudsc.c:25-27 defaults */
+  o->ngpus = 1; o->precision = CLOUDSC_FP64; o->variant = CLOUDSC_VARIANT_KSEG;
+  o->reps = 1; o->warmup = 1; o->tol = 1e-12;
+  int npos = 0;
+  long pos[3] = {0, 0, 0};
+  for (int i = 1; i < argc; i++) {
+    const char *a = argv[i];
+    const char *v = i + 1 < argc ? argv[i + 1] : NULL;
+#define NEEDV() do { if (!v) { fprintf(stderr, "%s needs a value\n", a); return -1; } i++; } while (0)
+    if (!strcmp(a, "--gpus")) { NEEDV(); o->ngpus = atoi(v); }
+    else if (!strcmp(a, "--precision")) {
+      NEEDV();
+      if (!strcmp(v, "fp64") || !strcmp(v, "dp")) o->precision = CLOUDSC_FP64;
+      else if (!strcmp(v, "fp32") || !strcmp(v, "sp")) o->precision = CLOUDSC_FP32;
+      else { fprintf(stderr, "bad precision %s\n", v); return -1; }
+    } else if (!strcmp(a, "--variant")) {
+      NEEDV();
+      if (!strcmp(v, "kseg")) o->variant = CLOUDSC_VARIANT_KSEG;
+      else if (!strcmp(v, "kcache")) o->variant = CLOUDSC_VARIANT_KCACHE;
+      else if (!strcmp(v, "scc")) o->variant = CLOUDSC_VARIANT_SCC;
+      else { fprintf(stderr, "bad variant %s\n", v); return -1; }
+    } else if (!strcmp(a, "--reps")) { NEEDV(); o->reps = atoi(v); }
+    else if (!strcmp(a, "--warmup")) { NEEDV(); o->warmup = atoi(v); }
+    else if (!strcmp(a, "--input")) { NEEDV(); o->input_h5 = v; }
+    else if (!strcmp(a, "--reference")) { NEEDV(); o->reference_h5 = v; }
+    else if (!strcmp(a, "--data")) { NEEDV(); o->data_dir = v; }
+    else if (!strcmp(a, "--tol")) { NEEDV(); o->tol = atof(v); o->tol_given = 1; }
+    else if (!strcmp(a, "--write-h5")) { NEEDV(); o->write_h5_dir = v; }
+    else if (!strcmp(a, "-h") || !strcmp(a, "--help")) return -1;
+    else if (a[0] == '-' && a[1] == '-') { fprintf(stderr, "unknown option %s\n", a); return -1; }
+    else {
+      if (npos >= 3) { fprintf(stderr, "too many arguments\n"); return -1; }
+      char *end;
+      pos[npos++] = strtol(a, &end, 10);
+      if (*end) { fprintf(stderr, "not a number: %s\n", a); return -1; }
+    }
+#undef NEEDV
+  }
+  if (npos != 0 && npos != 3) {
+    /* dwarf_cloudsc.c:45-48 */
+    printf("Calling c-cloudsc with the right number of arguments will work better ;-) \n");
+    return -1;
+  }
+  if (npos == 3) {
+    o->numomp = (int)pos[0]; o->ngptot = (int)pos[1]; o->nproma = (int)pos[2];
+    if (o->numomp <= 0) o->numomp = 1;
+  }
+  if (o->ngptot <= 0 || o->nproma <= 0 || o->nproma > 256 || o->ngpus <= 0 || o->reps <= 0 || o->warmup < 0) {
+    fprintf(stderr, "invalid sizes: ngptot %d nproma %d (1..256) gpus %d reps %d\n", o->ngptot, o->nproma,
+            o->ngpus, o->reps);
+    return -1;
+  }
+  return 0;
+}
+
+/* the raw dataset next to the executable: <exe dir>/../tests/golden/cloudsc100 */
+static void default_data_dir(char *out, size_t n) {
+  const char *env = getenv("CLOUDSC_DATA");
+  if (env && *env) { snprintf(out, n, "%s", env); return; }
+  char exe[PATH_MAX - 64];
+  ssize_t len = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+  if (len <= 0) { snprintf(out, n, "tests/golden/cloudsc100"); return; }
+  exe[len] = 0;
+  char *slash = strrchr(exe, '/');
+  if (slash) *slash = 0;
+  snprintf(out, n, "%s/../tests/golden/cloudsc100", exe);
+}
+
+static int exists(const char *p) { return access(p, R_OK) == 0; }
+
+static void *shard_main(void *arg) {
+  shard_t *s = (shard_t *)arg;
+  cloudsc_gpu_state_t *st = NULL;
+  s->rc = cloudsc_state_create(&st, s->device, s->precision, s->ngptot, s->nproma, s->col_offset, s->tmpl,
+                               s->params);
+  if (!s->rc && s->warmup > 0) {
+    float *w = (float *)malloc(sizeof(float) * s->warmup);
+    s->rc = w ? cloudsc_state_run(st, s->variant, s->warmup, w) : CLOUDSC_ENOMEM;
+    free(w);
+  }
+  if (!s->rc) s->rc = cloudsc_state_sync(st);
+  /* every shard reaches the barrier, also after an error, so nobody waits forever */
+  pthread_barrier_wait(s->barrier);
+  s->t_start = now();
+  if (!s->rc) s->rc = cloudsc_state_run(st, s->variant, s->reps, s->kernel_ms);
+  if (!s->rc) s->rc = cloudsc_state_sync(st);
+  s->t_end = now();
+  pthread_barrier_wait(s->barrier);
+  if (!s->rc && s->ref) s->rc = cloudsc_state_validate(st, s->ref, s->stats);
+  if (st) cloudsc_state_destroy(st);
+  return NULL;
+}
+
+/* ERROR_PRINT (validate_mod.F90:263-296 / cloudsc_validate.c:20-44) */
+static double print_error(const char *name, int ndim, const cloudsc_stats_t *s, int ngptot) {
+  const double eps = DBL_EPSILON;
+  double rel;
+  int iopt;
+  if (s->errsum < eps) { rel = 0.0; iopt = 1; }
+  else if (s->refsum < eps) { rel = s->errsum / (1.0 + s->refsum); iopt = 2; }
+  else { rel = s->errsum / s->refsum; iopt = 3; }
+  printf(" %20s %dD%d %20.13le %20.13le %20.13le %20.13le %20.13le %s\n", name, ndim, iopt, s->minval, s->maxval,
+         s->maxerr, s->errsum / (double)ngptot, 100.0 * rel, rel > 10.0 * eps ? " !!!!" : "     ");
+  return rel;
+}
+
+int main(int argc, char **argv) {
+  options_t o;
+  if (parse(argc, argv, &o)) { usage(argv[0]); return EXIT_FAILURE; }
+
+  /* ---- load the KLON-column state (HDF5 read-only, else raw) ---- */
+  cloudsc_dataset_t ds;
+  int rc;
+  const char *in_h5 = o.input_h5 ? o.input_h5 : (exists("input.h5") ? "input.h5" : NULL);
+  if (in_h5) {
+    const char *ref_h5 = o.reference_h5 ? o.reference_h5 : (exists("reference.h5") ? "reference.h5" : NULL);
+    rc = cloudsc_io_load_hdf5(in_h5, ref_h5, &ds);
+  } else {
+    char dir[PATH_MAX];
+    if (o.data_dir) snprintf(dir, sizeof(dir), "%s", o.data_dir);
+    else default_data_dir(dir, sizeof(dir));
+    rc = cloudsc_io_load_raw(dir, 1, &ds);
+    if (!rc && o.reference_h5) {
+      rc = cloudsc_io_load_hdf5_reference(o.reference_h5, &ds);     /* raw inputs, HDF5 reference */
+      if (!rc) {
+        size_t n = strlen(ds.source);
+        snprintf(ds.source + n, sizeof(ds.source) - n, " + HDF5 %s (read-only)", o.reference_h5);
+      }
+    }
+  }
+  if (rc) {
+    fprintf(stderr, "dwarf-cloudsc-amd: cannot load the input state: %s (%s)\n", cloudsc_strerror(rc),
+            cloudsc_io_last_error());
+    return EXIT_FAILURE;
+  }
+  if (o.write_h5_dir) {
+    char a[PATH_MAX], b[PATH_MAX];
+    snprintf(a, sizeof(a), "%s/input.h5", o.write_h5_dir);
+    snprintf(b, sizeof(b), "%s/reference.h5", o.write_h5_dir);
+    rc = cloudsc_io_write_hdf5(&ds, a, ds.has_reference ? b : NULL);
+    if (rc) fprintf(stderr, "write failed: %s\n", cloudsc_io_last_error());
+    else printf(" wrote %s%s%s\n", a, ds.has_reference ? " and " : "", ds.has_reference ? b : "");
+    cloudsc_io_free(&ds);
+    return rc ? EXIT_FAILURE : EXIT_SUCCESS;
+  }
+
+  int ndev = 0;
+  if ((rc = cloudsc_gpu_device_count(&ndev)) || ndev <= 0) {
+    fprintf(stderr, "dwarf-cloudsc-amd: no HIP device (%s)\n", rc ? cloudsc_strerror(rc) : "0 devices");
+    cloudsc_io_free(&ds);
+    return EXIT_FAILURE;
+  }
+  if (o.ngpus > ndev) {
+    fprintf(stderr, "dwarf-cloudsc-amd: --gpus %d but only %d device(s)\n", o.ngpus, ndev);
+    cloudsc_io_free(&ds);
+    return EXIT_FAILURE;
+  }
+
+  cloudsc_template_t tmpl;
+  cloudsc_reference_t ref;
+  cloudsc_io_template(&ds, &tmpl);
+  cloudsc_io_reference(&ds, &ref);
+  const int nblocks = o.ngptot / o.nproma + (o.ngptot % o.nproma ? 1 : 0);
+  printf(" CLOUDSC-AMD: %s, variant %s, %d device(s); state: %s (KLON=%d, KLEV=%d)\n",
+         o.precision == CLOUDSC_FP64 ? "fp64" : "fp32",
+         o.variant == CLOUDSC_VARIANT_KSEG ? "kseg" : o.variant == CLOUDSC_VARIANT_KCACHE ? "kcache" : "scc",
+         o.ngpus, ds.source, ds.klon, ds.klev);
+
+  /* ---- shard: block-aligned contiguous ranges of the global column index ---- */
+  shard_t *sh = (shard_t *)calloc((size_t)o.ngpus, sizeof(shard_t));
+  pthread_t *th = (pthread_t *)calloc((size_t)o.ngpus, sizeof(pthread_t));
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, (unsigned)o.ngpus);
+  const int blocks_per = nblocks / o.ngpus, extra = nblocks % o.ngpus;
+  long long col = 0;
+  int nused = 0;
+  for (int d = 0; d < o.ngpus; d++) {
+    const int nb = blocks_per + (d < extra ? 1 : 0);
+    long long cols = (long long)nb * o.nproma;
+    if (col + cols > o.ngptot) cols = o.ngptot - col;
+    if (cols <= 0) break;
+    shard_t *s = &sh[nused++];
+    s->device = d; s->ngptot = (int)cols; s->col_offset = col; s->nproma = o.nproma;
+    s->precision = o.precision; s->variant = o.variant; s->reps = o.reps; s->warmup = o.warmup;
+    s->tmpl = &tmpl; s->params = &ds.params; s->ref = ds.has_reference ? &ref : NULL; s->barrier = &bar;
+    s->kernel_ms = (float *)calloc((size_t)o.reps, sizeof(float));
+    col += cols;
+  }
+  if (nused != o.ngpus) {
+    pthread_barrier_destroy(&bar);
+    pthread_barrier_init(&bar, NULL, (unsigned)nused);
+  }
+  for (int d = 0; d < nused; d++) pthread_create(&th[d], NULL, shard_main, &sh[d]);
+  for (int d = 0; d < nused; d++) pthread_join(th[d], NULL);
+  pthread_barrier_destroy(&bar);
+
+  int failed = 0;
+  for (int d = 0; d < nused; d++)
+    if (sh[d].rc) {
+      fprintf(stderr, "dwarf-cloudsc-amd: device %d: %s (%s)\n", sh[d].device, cloudsc_strerror(sh[d].rc),
+              cloudsc_last_hip_error());
+      failed = 1;
+    }
+  if (failed) { cloudsc_io_free(&ds); return EXIT_FAILURE; }
+
+  /* ---- timing table (cloudsc_driver.c:233-262) ---- */
+  double t0 = sh[0].t_start, t1 = sh[0].t_end;
+  for (int d = 1; d < nused; d++) {
+    if (sh[d].t_start < t0) t0 = sh[d].t_start;
+    if (sh[d].t_end > t1) t1 = sh[d].t_end;
+  }
+  const double tdiff = t1 - t0;
+  const double cols_done = (double)o.ngptot * o.reps;
+  printf("     NUMOMP=%d, NGPTOT=%d, NPROMA=%d, NGPBLKS=%d\n", o.numomp, o.ngptot, o.nproma, nblocks);
+  printf(" Reference MFLOP count for 100 columns : %12.8f\n", 1.0e-06 * ZHPM);
+  printf(" %10s%10s%10s%10s%10s %4s : %10s%10s%10s\n", "NUMOMP", "NGPTOT", "#GP-cols", "#BLKS", "NPROMA", "tid#",
+         "Time(msec)", "MFlops/s", "col/s");
+  for (int d = 0; d < nused; d++) {
+    const double tl = sh[d].t_end - sh[d].t_start;
+    const int nbd = sh[d].ngptot / o.nproma + (sh[d].ngptot % o.nproma ? 1 : 0);
+    const double c = (double)sh[d].ngptot * o.reps;
+    printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d @ gpu#\n", o.numomp, o.ngptot, sh[d].ngptot, nbd, o.nproma,
+           sh[d].device, (int)(tl * 1000.), tl > 0 ? (int)(1.0e-06 * ZHPM * (c / 100.) / tl) : 0,
+           tl > 0 ? (int)(c / tl) : 0);
+  }
+  printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d TOTAL\n", o.numomp, o.ngptot, o.ngptot, nblocks, o.nproma, -1,
+         (int)(tdiff * 1000.), tdiff > 0 ? (int)(1.0e-06 * ZHPM * (cols_done / 100.) / tdiff) : 0,
+         tdiff > 0 ? (int)(cols_done / tdiff) : 0);
+  /* precise figures for scripts (the table above keeps the reference's integer format) */
+  double kmax = 0.0;
+  for (int d = 0; d < nused; d++) {
+    double k = 0.0;
+    for (int r = 0; r < o.reps; r++) k += sh[d].kernel_ms[r];
+    k /= o.reps;
+    if (k > kmax) kmax = k;
+  }
+  printf(" TIMING: steps=%d wall_ms_per_step=%.4f kernel_ms_per_step=%.4f columns_per_s=%.1f devices=%d\n", o.reps,
+         1e3 * tdiff / o.reps, kmax, cols_done / tdiff, nused);
+
+  /* ---- validation (cloudsc_validate.c:193-216, combined over devices) ---- */
+  int bad = 0;
+  if (ds.has_reference) {
+    printf(" %20s %s %20s %20s %20s %20s %20s\n", "Variable", "Dim", "MinValue", "MaxValue", "AbsMaxErr",
+           "AvgAbsErr/GP", "MaxRelErr-%");
+    const int gate = o.precision == CLOUDSC_FP64 || o.tol_given;
+    double worst = 0.0;
+    for (int f = 0; f < CLOUDSC_NVALID; f++) {
+      cloudsc_stats_t s = sh[0].stats[f];
+      for (int d = 1; d < nused; d++) {
+        const cloudsc_stats_t *q = &sh[d].stats[f];
+        s.minval = fmin(s.minval, q->minval);
+        s.maxval = fmax(s.maxval, q->maxval);
+        s.maxerr = fmax(s.maxerr, q->maxerr);
+        s.errsum += q->errsum;
+        s.refsum += q->refsum;
+      }
+      const int kind = cloudsc_io_ref_kind[f];
+      const double rel = print_error(cloudsc_io_print_names[f], kind == 3 ? 1 : kind == 2 ? 3 : 2, &s, o.ngptot);
+      if (rel > worst) worst = rel;
+      if (gate && !(rel <= o.tol)) bad++;
+    }
+    if (gate)
+      printf(" VALIDATION: %s (worst relative L1 error %.3e, gate %.1e, %d field(s) over)\n",
+             bad ? "FAILED" : "PASSED", worst, o.tol, bad);
+    else
+      printf(" VALIDATION: reported only (fp32 vs the fp64 reference; worst relative L1 error %.3e)\n", worst);
+  } else {
+    printf(" VALIDATION: skipped (no reference outputs loaded)\n");
+  }
+  for (int d = 0; d < nused; d++) free(sh[d].kernel_ms);
+  free(sh);
+  free(th);
+  cloudsc_io_free(&ds);
+  return bad ? EXIT_FAILURE : EXIT_SUCCESS;
+}

@@ -1,0 +1,200 @@
+"""Host plumbing of the dwarf driver (no GPU): the C dataset readers/writer of
+dwarf-p-cloudsc_amd/csrc/cloudsc_io.c through libcloudsc_io.so, and the
+dwarf-cloudsc-amd CLI paths that need no device.
+
+Pinned against the reference's own files: tests/golden/cloudsc100 holds the
+Serialbox arrays of the reference's data/, tests/golden/reference.h5 is
+config-files/reference.h5.  The HDF5 writer must reproduce that file exactly
+from the raw arrays (the input.h5 regeneration tool of SURVEY.md §8f-1)."""
+import ctypes as C
+import os
+import shutil
+import stat
+import subprocess
+
+import numpy as np
+import pytest
+
+import cloudsc_amd as ca
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "dwarf-p-cloudsc_amd")
+IO_LIB = os.path.join(PKG, "libcloudsc_io.so")
+DWARF = os.path.join(PKG, "dwarf-cloudsc-amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+REF_H5_UPSTREAM = "/root/reference/config-files/reference.h5"
+
+NIN = 28
+INPUT_NAMES = ["pt", "pq", "tendency_tmp_t", "tendency_tmp_q", "tendency_tmp_a", "tendency_tmp_cld", "pvfl",
+               "pvfi", "phrsw", "phrlw", "pvervel", "pap", "paph", "plsm", "ktype", "plu", "plude", "psnde",
+               "pmfu", "pmfd", "pa", "pclv", "psupsat", "plcrit_aer", "picrit_aer", "pre_ice", "pccn", "pnice"]
+
+
+class Dataset(C.Structure):
+    _fields_ = [("klon", C.c_int), ("klev", C.c_int), ("params", ca.Params),
+                ("inp", C.POINTER(C.c_double) * NIN), ("ktype", C.POINTER(C.c_int)),
+                ("ref", C.POINTER(C.c_double) * 21), ("has_reference", C.c_int), ("source", C.c_char * 512)]
+
+
+@pytest.fixture(scope="module")
+def io():
+    # the CLI links libcloudsc_amd.so; building it is __graft_entry__.build()'s job
+    if not os.path.exists(IO_LIB):
+        subprocess.check_call(["make", "-s", "-C", PKG, "libcloudsc_io.so"])
+    lib = C.CDLL(IO_LIB)
+    lib.cloudsc_io_load_raw.argtypes = [C.c_char_p, C.c_int, C.POINTER(Dataset)]
+    lib.cloudsc_io_load_hdf5.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Dataset)]
+    lib.cloudsc_io_load_hdf5_reference.argtypes = [C.c_char_p, C.POINTER(Dataset)]
+    lib.cloudsc_io_write_hdf5.argtypes = [C.POINTER(Dataset), C.c_char_p, C.c_char_p]
+    lib.cloudsc_io_free.argtypes = [C.POINTER(Dataset)]
+    lib.cloudsc_io_last_error.restype = C.c_char_p
+    return lib
+
+
+def need_hdf5(io):
+    if not io.cloudsc_io_hdf5_available():
+        pytest.skip("no libhdf5 on this host: %s" % io.cloudsc_io_last_error().decode())
+
+
+def arrays(d: Dataset):
+    """numpy copies of a loaded dataset, keyed like cloudsc_amd.Dataset"""
+    klev, klon = d.klev, d.klon
+    kinds = {**ca.INPUT_FIELDS, **ca.AEROSOL_FIELDS, **ca.INOUT_FIELDS}
+    inp = {}
+    for i, name in enumerate(INPUT_NAMES):
+        shp = ca.field_shape(kinds[name], klev, klon)
+        n = int(np.prod(shp))
+        if name == "ktype":
+            if d.ktype:
+                inp[name] = np.ctypeslib.as_array(d.ktype, (n,)).reshape(shp).copy()
+        elif d.inp[i]:
+            inp[name] = np.ctypeslib.as_array(d.inp[i], (n,)).reshape(shp).copy()
+    ref = {}
+    for i, (_, key) in enumerate(ca.VALIDATED):
+        if d.ref[i]:
+            shp = ca.field_shape(ca.ALL_FIELDS[key], klev, klon)
+            ref[key] = np.ctypeslib.as_array(d.ref[i], (int(np.prod(shp)),)).reshape(shp).copy()
+    return inp, ref
+
+
+def load_raw(io, path=os.path.join(GOLDEN, "cloudsc100")):
+    d = Dataset()
+    rc = io.cloudsc_io_load_raw(path.encode(), 1, C.byref(d))
+    assert rc == 0, io.cloudsc_io_last_error()
+    return d
+
+
+def test_raw_reader_matches_python_loader(io, ds):
+    d = load_raw(io)
+    try:
+        assert (d.klon, d.klev) == (ds.klon, ds.klev)
+        inp, ref = arrays(d)
+        for k, v in ds.inputs.items():
+            assert np.array_equal(inp[k], v), k
+        for k, v in ds.reference.items():
+            assert np.array_equal(ref[k], v), k
+        assert d.params.to_dict() == ca.Params.from_dict(ds.params).to_dict()
+    finally:
+        io.cloudsc_io_free(C.byref(d))
+
+
+def test_raw_reader_errors(io, tmp_path):
+    d = Dataset()
+    assert io.cloudsc_io_load_raw(str(tmp_path).encode(), 1, C.byref(d)) == -6     # no manifest
+    shutil.copytree(os.path.join(GOLDEN, "cloudsc100"), tmp_path / "ds")
+    with open(tmp_path / "ds" / "input_PT.dat", "r+b") as fh:                     # truncated field
+        fh.truncate(100)
+    assert io.cloudsc_io_load_raw(str(tmp_path / "ds").encode(), 1, C.byref(d)) == -6
+    assert b"input_PT.dat" in io.cloudsc_io_last_error()
+
+
+def test_hdf5_writer_reproduces_reference_h5(io, tmp_path):
+    """Raw arrays -> reference.h5 through our writer == the reference's file."""
+    need_hdf5(io)
+    d = load_raw(io)
+    try:
+        out = tmp_path / "reference.h5"
+        assert io.cloudsc_io_write_hdf5(C.byref(d), None, str(out).encode()) == 0, io.cloudsc_io_last_error()
+        for fixture in (os.path.join(GOLDEN, "reference.h5"), REF_H5_UPSTREAM):
+            if not os.path.exists(fixture):
+                continue
+            h5diff = shutil.which("h5diff") or "/opt/conda/bin/h5diff"
+            if os.path.exists(h5diff):
+                r = subprocess.run([h5diff, str(out), fixture], capture_output=True, text=True)
+                assert r.returncode == 0, r.stdout[-2000:]
+            # and through our own read-only reader
+            e = Dataset()
+            e.klon, e.klev = d.klon, d.klev
+            assert io.cloudsc_io_load_hdf5_reference(fixture.encode(), C.byref(e)) == 0
+            _, ref_a = arrays(d)
+            _, ref_b = arrays(e)
+            for k in ref_a:
+                assert np.array_equal(ref_a[k], ref_b[k]), k
+            io.cloudsc_io_free(C.byref(e))
+    finally:
+        io.cloudsc_io_free(C.byref(d))
+
+
+def test_hdf5_input_roundtrip_readonly(io, tmp_path):
+    """input.h5 written from the raw state reads back identically, from a
+    read-only file (the C reference opens it RDWR: load_state.c:499)."""
+    need_hdf5(io)
+    d = load_raw(io)
+    try:
+        inp_h5, ref_h5 = tmp_path / "input.h5", tmp_path / "reference.h5"
+        assert io.cloudsc_io_write_hdf5(C.byref(d), str(inp_h5).encode(), str(ref_h5).encode()) == 0
+        for p in (inp_h5, ref_h5):
+            os.chmod(p, stat.S_IRUSR | stat.S_IRGRP | stat.S_IROTH)
+        e = Dataset()
+        rc = io.cloudsc_io_load_hdf5(str(inp_h5).encode(), str(ref_h5).encode(), C.byref(e))
+        assert rc == 0, io.cloudsc_io_last_error()
+        a_in, a_ref = arrays(d)
+        b_in, b_ref = arrays(e)
+        assert a_in.keys() == b_in.keys() and a_ref.keys() == b_ref.keys()
+        for k in a_in:
+            assert np.array_equal(a_in[k], b_in[k]), k
+        for k in a_ref:
+            assert np.array_equal(a_ref[k], b_ref[k]), k
+        assert d.params.to_dict() == e.params.to_dict()
+        assert b"read-only" in e.source
+        io.cloudsc_io_free(C.byref(e))
+    finally:
+        io.cloudsc_io_free(C.byref(d))
+
+
+def test_hdf5_missing_dataset_reported(io, tmp_path):
+    need_hdf5(io)
+    d = load_raw(io)
+    try:
+        ref_only = tmp_path / "r.h5"
+        assert io.cloudsc_io_write_hdf5(C.byref(d), None, str(ref_only).encode()) == 0
+        e = Dataset()
+        # a reference file is not an input file: KLON exists, PT does not
+        assert io.cloudsc_io_load_hdf5(str(ref_only).encode(), None, C.byref(e)) == -6
+        assert b"/PT" in io.cloudsc_io_last_error()
+        assert io.cloudsc_io_load_hdf5(str(tmp_path / "nope.h5").encode(), None, C.byref(e)) == -6
+    finally:
+        io.cloudsc_io_free(C.byref(d))
+
+
+def test_cli_argument_errors():
+    """dwarf_cloudsc.c:45-48: wrong argument count -> message, EXIT_FAILURE;
+    needs no device."""
+    if not os.path.exists(DWARF):
+        pytest.skip("dwarf-cloudsc-amd not built (needs libcloudsc_amd.so: __graft_entry__.build())")
+    r = subprocess.run([DWARF, "1", "100"], capture_output=True, text=True)
+    assert r.returncode == 1 and "right number of arguments" in r.stdout
+    r = subprocess.run([DWARF, "1", "100", "300"], capture_output=True, text=True)    # nproma > 256
+    assert r.returncode == 1 and "invalid sizes" in r.stderr
+    r = subprocess.run([DWARF, "--variant", "nope"], capture_output=True, text=True)
+    assert r.returncode == 1
+
+
+def test_cli_write_h5(tmp_path, io):
+    """dwarf-cloudsc-amd --write-h5 regenerates input.h5 + reference.h5 (no device)."""
+    need_hdf5(io)
+    if not os.path.exists(DWARF):
+        pytest.skip("dwarf-cloudsc-amd not built")
+    r = subprocess.run([DWARF, "--write-h5", str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "input.h5").exists() and (tmp_path / "reference.h5").exists()
