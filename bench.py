@@ -69,59 +69,49 @@ def cpu_baseline(ds, ncols, nproma=32):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import cloudsc_amd as ca
+    import cloudsc_dist as cd
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
+    topo = cd.topology_from_env()
+    ctl = cd.Control(topo)               # gloo: barrier + max-over-ranks only
+    world, rank = topo.world, topo.rank
+    col_offset, ncols = cd.shard(rank, args.ngptot)
 
     prec = ca.FP64 if args.precision == "fp64" else ca.FP32
     variant = {"kseg": ca.VARIANT_KSEG, "kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC}[args.variant]
     ds = ca.load_dataset()
-    g = ca.GpuState(ds, args.ngptot, args.nproma, prec, device=local_rank,
-                    col_offset=rank * args.ngptot)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+    # one GPU per local rank (ranks beyond the device count share devices, e.g.
+    # a 2-rank rehearsal on a 1-GPU box)
+    device = topo.local_rank % ca.device_count()
+    g = ca.GpuState(ds, ncols, args.nproma, prec, device=device, col_offset=col_offset)
 
     if args.warmup > 0:
         g.run(variant, args.warmup)
-    barrier()
     g.sync()
+    ctl.barrier()
     t0 = time.perf_counter()
     kernel_ms = g.run(variant, args.steps)      # plude restore + launch per step; events around launch
     g.sync()
     t1 = time.perf_counter()
-    barrier()
-    wall = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    ctl.barrier()
+    wall = ctl.max(t1 - t0)
+    k_avg_ms = ctl.max(float(np.mean(kernel_ms)))
 
-    # validation of the last step against reference.h5 (device-side statistics)
-    stats = g.validate()
+    # validation of the last step against reference.h5 (device-side statistics, combined over ranks)
+    stats = ctl.gather_stats(g.validate())
     worst = 0.0
     for (mn, mx, maxerr, errsum, refsum) in stats:
         worst = max(worst, errsum / refsum if refsum > 0 else errsum)
     g.close()
 
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        ctl.close()
         return
 
     total_cols = args.ngptot * world
     ms_per_step = 1e3 * wall / args.steps
     value = total_cols * args.steps / wall
-    k_avg_ms = float(np.mean(kernel_ms))
     bpc = BYTES_PER_COL[prec]
     achieved = bpc * args.ngptot / (k_avg_ms * 1e-3) / 1e9
     traffic = None
@@ -163,8 +153,7 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(ds, min(args.cpu_sample, args.ngptot))
     print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    ctl.close()
 
 
 if __name__ == "__main__":

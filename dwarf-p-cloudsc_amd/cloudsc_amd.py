@@ -345,6 +345,13 @@ def gpu_lib(path: Optional[str] = None):
     return lib
 
 
+def device_count() -> int:
+    """Visible HIP devices (through the library; raises if it is missing)."""
+    n = C.c_int(0)
+    check(gpu_lib().cloudsc_gpu_device_count(C.byref(n)))
+    return n.value
+
+
 def check(rc: int) -> None:
     if rc != 0:
         lib = gpu_lib()

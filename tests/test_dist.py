@@ -1,0 +1,99 @@
+"""Multi-process control path of bench.py on the CPU (gloo, world size 2):
+weak-scaling shards, barrier + max-over-ranks, combined validation statistics,
+and the sharding semantics themselves -- rank r's columns, computed by the
+oracle with the GLOBAL g % klon map, equal the matching slice of an unsharded
+run bit for bit (no data-path collective exists to get this wrong later)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import cloudsc_amd as ca
+import cloudsc_dist as cd
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    try:
+        topo = cd.topology_from_env()
+        ctl = cd.Control(topo)
+        ctl.barrier()
+        wall = ctl.max(0.5 + rank)                       # the slowest rank defines the step time
+        off, n = cd.shard(topo.rank, 1000)
+        # per-rank validation partials: field 0 gets rank-dependent numbers
+        stats = [[-1.0 - rank, 1.0 + rank, 0.1 * (rank + 1), 2.0, 10.0]] + [[0.0, 0.0, 0.0, 0.0, 1.0]] * 20
+        comb = ctl.gather_stats(stats)
+        ctl.barrier()
+        ctl.close()
+        q.put((rank, wall, off, n, comb[0], len(comb)))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, "error", repr(e)))
+
+
+def test_gloo_world2_control_path():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r
+    assert [r[1] for r in res] == [1.5, 1.5]
+    assert [(r[2], r[3]) for r in res] == [(0, 1000), (1000, 1000)]
+    for r in res:
+        assert r[4] == (-2.0, 2.0, 0.2, 4.0, 20.0) and r[5] == 21
+
+
+def test_single_rank_control_is_noop():
+    ctl = cd.Control(cd.Topology(0, 1, 0))
+    ctl.barrier()
+    assert ctl.max(3.0) == 3.0
+    st = [[1.0, 2.0, 3.0, 4.0, 5.0]]
+    assert ctl.gather_stats(st) == [(1.0, 2.0, 3.0, 4.0, 5.0)]
+
+
+def test_split_blocks_covers_columns():
+    for ngptot, nproma, parts in [(163840, 128, 8), (1000, 128, 3), (100, 32, 8), (1310720, 128, 8)]:
+        sp = cd.split_blocks(ngptot, nproma, parts)
+        assert sp[0][0] == 0 and sum(n for _, n in sp) == ngptot
+        for (o1, n1), (o2, _) in zip(sp, sp[1:]):
+            assert o1 + n1 == o2 and o2 % nproma == 0
+
+
+def test_sharded_oracle_equals_unsharded(ds, oracle_mod):
+    """Weak-scaling semantics: two 256-column shards == one 512-column run."""
+    full, _ = oracle_mod.run_oracle(ds, 512, 128)
+    ref = ca.state_outputs_to_template(full.arrays, 512)
+    for rank in range(2):
+        off, n = cd.shard(rank, 256)
+        part, _ = oracle_mod.run_oracle(ds, n, 128, col_offset=off)
+        out = ca.state_outputs_to_template(part.arrays, n)
+        for _, k in ca.VALIDATED:
+            assert np.array_equal(out[k], ref[k][..., off:off + n]), (rank, k)
+
+
+def test_combine_stats_matches_unsharded(ds):
+    """Host-side combination of per-shard ERROR_PRINT partials equals the
+    statistics of the whole field (sums up to rounding)."""
+    rng = np.random.default_rng(7)
+    for _, k in ca.VALIDATED[:5]:
+        ref = ds.reference[k]
+        out = ref * (1 + 1e-12 * rng.standard_normal(ref.shape))
+        whole = ca.field_stats(out, ref)
+        halves = [ca.field_stats(out[..., :50], ref[..., :50]), ca.field_stats(out[..., 50:], ref[..., 50:])]
+        comb = cd.combine_stats([[h] for h in halves])[0]
+        assert comb[:3] == whole[:3]
+        assert comb[3] == pytest.approx(whole[3], rel=1e-12) and comb[4] == pytest.approx(whole[4], rel=1e-12)
