@@ -96,6 +96,55 @@ __device__ __forceinline__ real cl_exp(real x) {
 #endif
 }
 
+// Division.  The IEEE sequence hipcc emits for a / b is
+//   div_scale(b), div_scale(a), rcp, 2 Newton steps (fp64; 1 in fp32), q = a*r,
+//   residual fma, div_fmas (= fma(residual, r, q) unless div_scale rescaled),
+//   div_fixup (inf / nan / zero operands)
+// -- 11 instructions.  cl_div is the same arithmetic without the range
+// scaling and the special-case fix-up: 8 instructions, and the reciprocal of a
+// repeated divisor is shared (CSE).  div_scale only rescales operands whose
+// exponents are near the ends of the range (quotient or divisor beyond about
+// 2^+-1000, denormals), and the fix-up only changes non-finite or zero
+// divisors, so for every finite, normal-range operand pair the result is
+// bit-identical to a / b (correctly rounded).  CLOUDSC's divisions are all
+// guarded (divisors are max(x, eps), 1 + positive sums, or branch-protected
+// ratios of physical quantities), and the A/B identity check
+// (tools/ab_compare.py: reference state, scenarios, random perturbations,
+// NSSOPT, aerosol flags, fp32, 163840 columns) confirms identical output bits.
+// CLOUDSC_IEEE_DIV restores the plain operator.
+template <typename real>
+__device__ __forceinline__ real cl_div(real n, real d);
+template <>
+__device__ __forceinline__ double cl_div<double>(double n, double d) {
+#ifdef CLOUDSC_IEEE_DIV
+  return n / d;
+#else
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = n * r;
+  const double rem = __builtin_fma(-d, q, n);
+  return __builtin_fma(rem, r, q);
+#endif
+}
+template <>
+__device__ __forceinline__ float cl_div<float>(float n, float d) {
+#ifdef CLOUDSC_IEEE_DIV
+  return n / d;
+#else
+  float r = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, r, 1.0f);
+  r = __builtin_fmaf(e, r, r);
+  float q = n * r;
+  float rem = __builtin_fmaf(-d, q, n);
+  q = __builtin_fmaf(rem, r, q);
+  rem = __builtin_fmaf(-d, q, n);
+  return __builtin_fmaf(rem, r, q);
+#endif
+}
+
 // FOEALFA (src/common/include/fcttre.func.h; inlined at cloudsc_c.c:588,831,1162-1174)
 template <typename real, typename P>
 __device__ __forceinline__ real foealfa(const P& c, real t) {
@@ -103,15 +152,15 @@ __device__ __forceinline__ real foealfa(const P& c, real t) {
   return fmin(R(1.0), x * x);            // pow(x,2) == x*x (both rounded once)
 }
 template <typename real, typename P>
-__device__ __forceinline__ real exp_liq(const P& c, real t) { return cl_exp<real>((c.r3les * (t - c.rtt)) / (t - c.r4les)); }
+__device__ __forceinline__ real exp_liq(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3les * (t - c.rtt), t - c.r4les)); }
 template <typename real, typename P>
-__device__ __forceinline__ real exp_ice(const P& c, real t) { return cl_exp<real>((c.r3ies * (t - c.rtt)) / (t - c.r4ies)); }
+__device__ __forceinline__ real exp_ice(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3ies * (t - c.rtt), t - c.r4ies)); }
 
 // alfa*R5ALVCP/(T-R4LES)^2 + (1-alfa)*R5ALSCP/(T-R4IES)^2 (cloudsc_c.c:1166,1220)
 template <typename real, typename P>
 __device__ __forceinline__ real foedem_term(const P& c, real t, real alfa) {
   real dl = t - c.r4les, di = t - c.r4ies;
-  return ((alfa * c.r5alvcp) * (R(1.0) / (dl * dl))) + (((R(1.0) - alfa) * c.r5alscp) * (R(1.0) / (di * di)));
+  return ((alfa * c.r5alvcp) * cl_div<real>(R(1.0), dl * dl)) + (((R(1.0) - alfa) * c.r5alscp) * cl_div<real>(R(1.0), di * di));
 }
 
 }  // namespace cloudsc

@@ -251,6 +251,8 @@ int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma,
     case 21: hipLaunchKernelGGL((kcache_entry<real, 2, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
     case 30: hipLaunchKernelGGL((kcache_entry<real, 3, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
     case 31: hipLaunchKernelGGL((kcache_entry<real, 3, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    case 40: hipLaunchKernelGGL((kcache_entry<real, 4, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+    case 41: hipLaunchKernelGGL((kcache_entry<real, 4, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
     default: return CLOUDSC_EINVAL;
   }
   return CLOUDSC_OK;
@@ -317,6 +319,8 @@ int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& p
     case 21: return launch_kseg_cfg<real, 2, 1, AER>(st, a, pa, nproma, nitems);
     case 30: return launch_kseg_cfg<real, 3, 0, AER>(st, a, pa, nproma, nitems);
     case 31: return launch_kseg_cfg<real, 3, 1, AER>(st, a, pa, nproma, nitems);
+    case 40: return launch_kseg_cfg<real, 4, 0, AER>(st, a, pa, nproma, nitems);
+    case 41: return launch_kseg_cfg<real, 4, 1, AER>(st, a, pa, nproma, nitems);
     default: return CLOUDSC_EINVAL;
   }
 }

@@ -219,19 +219,19 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     const real pap_k = in.pap;
     // saturation values (:583-609)
     const real e_liq = exp_liq<real>(c, ztp1), e_ice = exp_ice<real>(c, ztp1);
-    const real zfoeewmt = fmin((c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)) / pap_k, R(0.5));
-    const real zqsmix = zfoeewmt / (R(1.0) - c.retv * zfoeewmt);
+    const real zfoeewmt = fmin(cl_div((c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)), pap_k), R(0.5));
+    const real zqsmix = cl_div(zfoeewmt, (R(1.0) - c.retv * zfoeewmt));
     const real zalfa_d = fmax(R(0.0), copysign(R(1.0), ztp1 - c.rtt));
-    real zfoeew = fmin((zalfa_d * (c.r2es * e_liq) + (R(1.0) - zalfa_d) * (c.r2es * e_ice)) / pap_k, R(0.5));
+    real zfoeew = fmin(cl_div((zalfa_d * (c.r2es * e_liq) + (R(1.0) - zalfa_d) * (c.r2es * e_ice)), pap_k), R(0.5));
     zfoeew = fmin(R(0.5), zfoeew);
-    const real zqsice = zfoeew / (R(1.0) - c.retv * zfoeew);
-    const real zfoeeliqt = fmin((c.r2es * e_liq) / pap_k, R(0.5));
-    const real zqsliq = zfoeeliqt / (R(1.0) - c.retv * zfoeeliqt);
+    const real zqsice = cl_div(zfoeew, (R(1.0) - c.retv * zfoeew));
+    const real zfoeeliqt = fmin(cl_div((c.r2es * e_liq), pap_k), R(0.5));
+    const real zqsliq = cl_div(zfoeeliqt, (R(1.0) - c.retv * zfoeeliqt));
     // liquid/ice fractions (:628-636)
     const real zli = zqx[QL] + zqx[QI];
     real zliqfrac = R(0.0), zicefrac = R(0.0);
     if (zli > c.rlmin) {
-      zliqfrac = zqx[QL] / zli;
+      zliqfrac = cl_div(zqx[QL], zli);
       zicefrac = R(1.0) - zliqfrac;
     }
 
@@ -257,22 +257,22 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 
     // 3.0 derived variables (:799-841)
     const real zdp = nb.paph_n - nb.paph_k;
-    const real zgdp = c.rg / zdp;
-    const real zrho = pap_k / (c.rd * ztp1);
+    const real zgdp = cl_div(c.rg, zdp);
+    const real zrho = cl_div(pap_k, (c.rd * ztp1));
     const real zdtgdp = c.ptsphy * zgdp;
     const real zrdtgdp = zdp * c.zinv_tsrg;
     real zfacw, zfaci, zfac, zcor;
-    { const real d = ztp1 - c.r4les; zfacw = c.r5les / (d * d); }
-    { const real d = ztp1 - c.r4ies; zfaci = c.r5ies / (d * d); }
-    zcor = R(1.0) / (R(1.0) - c.retv * zfoeew);
+    { const real d = ztp1 - c.r4les; zfacw = cl_div(c.r5les, (d * d)); }
+    { const real d = ztp1 - c.r4ies; zfaci = cl_div(c.r5ies, (d * d)); }
+    zcor = cl_div(R(1.0), (R(1.0) - c.retv * zfoeew));
     const real zdqsicedt = (zfaci * zcor) * zqsice;
     const real zcorqsice = R(1.0) + c.ralsdcp * zdqsicedt;
     zfac = zfoealfa * zfacw + (R(1.0) - zfoealfa) * zfaci;
-    zcor = R(1.0) / (R(1.0) - c.retv * zfoeewmt);
+    zcor = cl_div(R(1.0), (R(1.0) - c.retv * zfoeewmt));
     const real zdqsmixdt = (zfac * zcor) * zqsmix;
     const real zcorqsmix = R(1.0) + (zfoealfa * c.ralvdcp + (R(1.0) - zfoealfa) * c.ralsdcp) * zdqsmixdt;
-    const real zevaplimmix = fmax((zqsmix - zqx[QV]) / zcorqsmix, R(0.0));
-    real ztmpa = R(1.0) / fmax(za, zepsec);
+    const real zevaplimmix = fmax(cl_div((zqsmix - zqx[QV]), zcorqsmix), R(0.0));
+    real ztmpa = cl_div(R(1.0), fmax(za, zepsec));
     real zliqcld = zqx[QL] * ztmpa;
     real zicecld = zqx[QI] * ztmpa;
     real zlicld = zliqcld + zicecld;
@@ -282,7 +282,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     if (zqx[QI] < c.rlmin) { sa_iv = zqx[QI]; }
 
     // 3.1 ice supersaturation adjustment (:874-954)
-    const real zfokoop = fmin(c.rkoop1 - c.rkoop2 * ztp1, (c.r2es * e_liq) * R(1.0) / (c.r2es * e_ice));
+    const real zfokoop = fmin(c.rkoop1 - c.rkoop2 * ztp1, cl_div((c.r2es * e_liq) * R(1.0), (c.r2es * e_ice)));
     if (c.nssopt == 0 || ztp1 >= c.rtt) {
       zfac = R(1.0);
       zfaci = R(1.0);
@@ -292,10 +292,10 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     }
     real zsupsat;
     if (za > c.one_m_ramin) {
-      zsupsat = fmax((zqx[QV] - zfac * zqsice) / zcorqsice, R(0.0));
+      zsupsat = fmax(cl_div((zqx[QV] - zfac * zqsice), zcorqsice), R(0.0));
     } else {
-      const real zqp1env = (zqx[QV] - za * zqsice) / fmax(R(1.0) - za, zepsilon);
-      zsupsat = fmax(((R(1.0) - za) * (zqp1env - zfac * zqsice)) / zcorqsice, R(0.0));
+      const real zqp1env = cl_div((zqx[QV] - za * zqsice), fmax(R(1.0) - za, zepsilon));
+      zsupsat = fmax(cl_div(((R(1.0) - za) * (zqp1env - zfac * zqsice)), zcorqsice), R(0.0));
     }
     const bool warm_homo = ztp1 > c.rthomo;
     if (zsupsat > zepsec) { CLOUDSC_BRANCH_COUNT(0);
@@ -317,7 +317,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     if (k < klev - 1) {
       plude_k = plude_k * zdtgdp;
       if (nb.plu_n > zepsec && plude_k > c.rlmin) {
-        zsolac = zsolac + plude_k / nb.plu_n;
+        zsolac = zsolac + cl_div(plude_k, nb.plu_n);
         conv_src_l = zfoealfa * plude_k;
         conv_src_i = (R(1.0) - zfoealfa) * plude_k;
         sa_ll = sa_ll + conv_src_l;
@@ -336,7 +336,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       const real zlcust_i = zmf * cs.qxnm1_i;
       conv_src_l = conv_src_l + zlcust_l;
       conv_src_i = conv_src_i + zlcust_i;
-      const real zdtdp = ((c.zrdcp * R(0.5)) * (cs.t_prev + ztp1)) / nb.paph_k;
+      const real zdtdp = cl_div(((c.zrdcp * R(0.5)) * (cs.t_prev + ztp1)), nb.paph_k);
       const real zdtforc = zdtdp * (pap_k - cs.pap_prev);
       const real zdqs = (cs.zanewm1 * zdtforc) * zdqsmixdt;
       real zlfinalsum = R(0.0);
@@ -374,7 +374,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       real zleros = za * ze;
       zleros = fmin(zleros, zevaplimmix);
       zleros = fmin(zleros, zli);
-      const real zaeros = zleros / zlicld;
+      const real zaeros = cl_div(zleros, zlicld);
       zsolac = zsolac - zaeros;
       sa_lv = sa_lv + zliqfrac * zleros;
       sa_iv = sa_iv + zicefrac * zleros;
@@ -383,7 +383,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // 3.4 condensation/evaporation due to dqsat/dt: two Newton steps (:1137-1182)
     real zdqs;
     {
-      const real zdtdp = (c.zrdcp * ztp1) / pap_k;
+      const real zdtdp = cl_div((c.zrdcp * ztp1), pap_k);
       const real zdpmxdt = zdp * c.zqtmst;
       const real zmfdn = (k < klev - 1) ? nb.pmfu_n + nb.pmfd_n : R(0.0);
       real zwtot = in.pvervel + c.half_rg * (nb.pmfu_k + nb.pmfd_k + zmfdn);
@@ -393,15 +393,15 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       const real zdtforc = (zdtdp * zwtot) * c.ptsphy + zdtdiab;
       real tt = fmax(ztp1 + zdtforc, R(160.0));
       real qsm = zqsmix;
-      const real zqp = R(1.0) / pap_k;
+      const real zqp = cl_div(R(1.0), pap_k);
   #pragma unroll
       for (int it = 0; it < 2; it++) {
         const real a = foealfa<real>(c, tt);
         real zqsat = (c.r2es * (a * exp_liq<real>(c, tt) + (R(1.0) - a) * exp_ice<real>(c, tt))) * zqp;
         zqsat = fmin(R(0.5), zqsat);
-        const real zcor2 = R(1.0) / (R(1.0) - c.retv * zqsat);
+        const real zcor2 = cl_div(R(1.0), (R(1.0) - c.retv * zqsat));
         zqsat = zqsat * zcor2;
-        const real zcond = (qsm - zqsat) / (R(1.0) + (zqsat * zcor2) * foedem_term<real>(c, tt, a));
+        const real zcond = cl_div((qsm - zqsat), (R(1.0) + (zqsat * zcor2) * foedem_term<real>(c, tt, a)));
         tt = tt + (a * c.ralvdcp + (R(1.0) - a) * c.ralsdcp) * zcond;
         qsm = qsm - zcond;
       }
@@ -421,10 +421,10 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       real zlcond1 = fmax(-zdqs, R(0.0));
       real zcdmax;
       if (za > R(0.99)) {
-        const real zcor3 = R(1.0) / (R(1.0) - c.retv * zqsmix);
-        zcdmax = (zqx[QV] - zqsmix) / (R(1.0) + (zcor3 * zqsmix) * foedem_term<real>(c, ztp1, zfoealfa));
+        const real zcor3 = cl_div(R(1.0), (R(1.0) - c.retv * zqsmix));
+        zcdmax = cl_div((zqx[QV] - zqsmix), (R(1.0) + (zcor3 * zqsmix) * foedem_term<real>(c, ztp1, zfoealfa)));
       } else {
-        zcdmax = (zqx[QV] - za * zqsmix) / za;
+        zcdmax = cl_div((zqx[QV] - za * zqsmix), za);
       }
       zlcond1 = fmax(fmin(zlcond1, zcdmax), R(0.0));
       zlcond1 = za * zlcond1;
@@ -436,14 +436,14 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // 3.4b(2) generation of new clouds (:1253-1363)
     if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) { CLOUDSC_BRANCH_COUNT(5);
       real zrhc = c.ramid;
-      const real zsigk = pap_k / cc.paph_sfc;
+      const real zsigk = cl_div(pap_k, cc.paph_sfc);
       if (zsigk > R(0.8)) {
-        const real s = (zsigk - R(0.8)) / R(0.2);
+        const real s = cl_div((zsigk - R(0.8)), R(0.2));
         zrhc = c.ramid + (R(1.0) - c.ramid) * (s * s);
       }
       real zqe = R(0.0);
       if (c.nssopt == 0 || c.nssopt == 1) {
-        zqe = (zqx[QV] - za * zqsice) / fmax(zepsec, R(1.0) - za);
+        zqe = cl_div((zqx[QV] - za * zqsice), fmax(zepsec, R(1.0) - za));
         zqe = fmax(R(0.0), zqe);
       } else if (c.nssopt == 2) {
         zqe = zqx[QV];
@@ -452,10 +452,10 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       }
       const real zfacn = (c.nssopt == 0 || ztp1 >= c.rtt) ? R(1.0) : zfokoop;
       if (zqe >= zqsice * zfacn * zrhc && zqe < zqsice * zfacn) { CLOUDSC_BRANCH_COUNT(6);
-        real zacond = -((R(1.0) - za) * zfacn) * zdqs / fmax(R(2.0) * (zfacn * zqsice - zqe), zepsec);
+        real zacond = cl_div(-((R(1.0) - za) * zfacn) * zdqs, fmax(R(2.0) * (zfacn * zqsice - zqe), zepsec));
         zacond = fmin(zacond, R(1.0) - za);
         real zlcond2 = -(zfacn * zdqs) * R(0.5) * zacond;
-        const real zzdl = (R(2.0) * (zfacn * zqsice - zqe)) / fmax(zepsec, R(1.0) - za);
+        const real zzdl = cl_div((R(2.0) * (zfacn * zqsice - zqe)), fmax(zepsec, R(1.0) - za));
         if (zdqs * zfacn < -zzdl) {
           const real zlcondlim = ((za - R(1.0)) * zfacn) * zdqs - zfacn * zqsice + zqx[QV];
           zlcond2 = fmin(zlcond2, zlcondlim);
@@ -475,26 +475,26 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 
     // 3.7 growth of ice by vapour deposition, Rotstayn (:1382-1447)
     if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
-    else cs.zcldtopdist = cs.zcldtopdist + zdp / (zrho * c.rg);
+    else cs.zcldtopdist = cs.zcldtopdist + cl_div(zdp, (zrho * c.rg));
     if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) { CLOUDSC_BRANCH_COUNT(7);
-      const real zvpice = ((c.r2es * e_ice) * c.rv) / c.rd;
+      const real zvpice = cl_div(((c.r2es * e_ice) * c.rv), c.rd);
       const real zvpliq = zvpice * zfokoop;
-      const real zicenuclei = R(1000.0) * cl_exp<real>((R(12.96) * (zvpliq - zvpice)) / zvpliq - R(0.639));
-      const real zadd = (c.rlstt * (c.rlstt / (c.rv * ztp1) - R(1.0))) / (R(0.024) * ztp1);
-      const real zbdd = ((c.rv * ztp1) * pap_k) / (R(2.21) * zvpice);
-      const real zcvds = ((R(7.8) * cl_pow<real>(zicenuclei / zrho, R(0.666))) * (zvpliq - zvpice)) / ((R(8.87) * (zadd + zbdd)) * zvpice);
-      const real zice0 = fmax(zicecld, (zicenuclei * c.riceinit) / zrho);
+      const real zicenuclei = R(1000.0) * cl_exp<real>(cl_div((R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
+      const real zadd = cl_div((c.rlstt * (cl_div(c.rlstt, (c.rv * ztp1)) - R(1.0))), (R(0.024) * ztp1));
+      const real zbdd = cl_div(((c.rv * ztp1) * pap_k), (R(2.21) * zvpice));
+      const real zcvds = cl_div(((R(7.8) * cl_pow<real>(cl_div(zicenuclei, zrho), R(0.666))) * (zvpliq - zvpice)), ((R(8.87) * (zadd + zbdd)) * zvpice));
+      const real zice0 = fmax(zicecld, cl_div((zicenuclei * c.riceinit), zrho));
       const real zinew = cl_pow<real>((R(0.666) * zcvds) * c.ptsphy + cl_pow<real>(zice0, R(0.666)), R(1.5));
       real zdepos = fmax(za * (zinew - zice0), R(0.0));
       zdepos = fmin(zdepos, zqxfg[QL]);
-      const real zinfactor = fmin(zicenuclei / R(15000.0), R(1.0));
-      zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cs.zcldtopdist / c.rdepliqrefdepth), R(1.0));
+      const real zinfactor = fmin(cl_div(zicenuclei, R(15000.0)), R(1.0));
+      zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cl_div(cs.zcldtopdist, c.rdepliqrefdepth)), R(1.0));
       sa_li = sa_li + zdepos;
       zqxfg[QI] = zqxfg[QI] + zdepos; zqxfg[QL] = zqxfg[QL] - zdepos;
     }
 
     // 4. revise in-cloud condensate (:1528-1533)
-    ztmpa = R(1.0) / fmax(za, zepsec);
+    ztmpa = cl_div(R(1.0), fmax(za, zepsec));
     zliqcld = zqxfg[QL] * ztmpa;
     zicecld = zqxfg[QI] * ztmpa;
     zlicld = zliqcld + zicecld;
@@ -513,11 +513,11 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // precip cover overlap, MAX-RAN (:1594-1611)
     real zcovpclr, zraincld, zsnowcld;
     if (zqpretot > zepsec) { CLOUDSC_BRANCH_COUNT(8);
-      cs.zcovptot = R(1.0) - (R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)) / (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6)));
+      cs.zcovptot = R(1.0) - cl_div((R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)), (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6))));
       cs.zcovptot = fmax(cs.zcovptot, c.rcovpmin);
       zcovpclr = fmax(R(0.0), cs.zcovptot - za);
-      zraincld = zqxfg[QR] / cs.zcovptot;
-      zsnowcld = zqxfg[QS] / cs.zcovptot;
+      zraincld = cl_div(zqxfg[QR], cs.zcovptot);
+      zsnowcld = cl_div(zqxfg[QS], cs.zcovptot);
       cs.zcovpmax = fmax(cs.zcovptot, cs.zcovpmax);
     } else {
       zraincld = R(0.0); zsnowcld = R(0.0); cs.zcovptot = R(0.0); zcovpclr = R(0.0); cs.zcovpmax = R(0.0);
@@ -530,9 +530,9 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       real zlcrit = c.rlcritsnow;
       if (c.laericeauto) {
         zlcrit = in.picrit_aer;
-        zzco = zzco * cl_pow<real>(c.rnice / in.pnice, R(0.333));
+        zzco = zzco * cl_pow<real>(cl_div(c.rnice, in.pnice), R(0.333));
       }
-      const real r = zicecld / zlcrit;
+      const real r = cl_div(zicecld, zlcrit);
       sb_is = sb_is + zzco * (R(1.0) - cl_exp<real>(-(r * r)));
     }
     // 4.3b warm rain, Khairoutdinov and Kogan 2000 (:1644-1761)
@@ -554,7 +554,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     }
     // riming of snow by cloud water (:1768-1808)
     if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) { CLOUDSC_BRANCH_COUNT(12);
-      const real zfallcorr = cl_pow<real>(c.rdensref / zrho, R(0.4));
+      const real zfallcorr = cl_pow<real>(cl_div(c.rdensref, zrho), R(0.4));
       real zsnowrime = ((((R(0.3) * cs.zcovptot) * c.ptsphy) * c.rcl_const7s) * zfallcorr) *
                        cl_pow<real>((zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
       zsnowrime = fmin(zsnowrime, R(1.0));
@@ -566,17 +566,17 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     if (zicetot > zepsec && ztp1 > c.rtt) { CLOUDSC_BRANCH_COUNT(13);
       const real zsubsat = fmax(zqsice - zqx[QV], R(0.0));
       const real ztdmtw0 = ztp1 - c.rtt - zsubsat * (ztw1 + ztw2 * (pap_k - ztw3) - ztw4 * (ztp1 - ztw5));
-      const real zcons1 = fabs((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)) / c.rtaumel);
+      const real zcons1 = fabs(cl_div((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)), c.rtaumel));
       const real zmeltmax = fmax((ztdmtw0 * zcons1) * c.zrldcp, R(0.0));
       if (zmeltmax > zepsec) {
         {   // ice -> rain
-          const real zalfa = zqxfg[QI] / zicetot;
+          const real zalfa = cl_div(zqxfg[QI], zicetot);
           const real zmelt = fmin(zqxfg[QI], zalfa * zmeltmax);
           zqxfg[QI] = zqxfg[QI] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
           sa_ir = sa_ir + zmelt;
         }
         {   // snow -> rain
-          const real zalfa = zqxfg[QS] / zicetot;
+          const real zalfa = cl_div(zqxfg[QS], zicetot);
           const real zmelt = fmin(zqxfg[QS], zalfa * zmeltmax);
           zqxfg[QS] = zqxfg[QS] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
           sa_sr = sa_sr + zmelt;
@@ -588,17 +588,17 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     if (zqx[QR] > zepsec) { CLOUDSC_BRANCH_COUNT(14);
       if (cold && cs.t_prev > c.rtt) {
         const real tot = fmax(zqx[QS] + zqx[QR], zepsec);
-        cs.rainfrac = zqx[QR] / tot;
+        cs.rainfrac = cl_div(zqx[QR], tot);
       }
       if (ztp1 < c.rtt) {
         real zfrzmax;
         if (cs.rainfrac > R(0.8)) {
-          const real zlambda = cl_pow<real>(c.rcl_fac1 / (zrho * zqx[QR]), c.rcl_fac2);
+          const real zlambda = cl_pow<real>(cl_div(c.rcl_fac1, (zrho * zqx[QR])), c.rcl_fac2);
           const real ztemp = c.rcl_fzrab * (ztp1 - c.rtt);
-          const real zfrz = ((c.ptsphy * (c.rcl_const5r / zrho)) * (cl_exp<real>(ztemp) - R(1.0))) * cl_pow<real>(zlambda, c.rcl_const6r);
+          const real zfrz = ((c.ptsphy * (cl_div(c.rcl_const5r, zrho))) * (cl_exp<real>(ztemp) - R(1.0))) * cl_pow<real>(zlambda, c.rcl_const6r);
           zfrzmax = fmax(zfrz, R(0.0));
         } else {
-          const real zcons1 = fabs((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))) / c.rtaumel);
+          const real zcons1 = fabs(cl_div((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))), c.rtaumel));
           zfrzmax = fmax(((c.rtt - ztp1) * zcons1) * c.zrldcp, R(0.0));
         }
         if (zfrzmax > zepsec) {
@@ -616,45 +616,45 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     }
 
     // 4.5 evaporation of rain, Abel and Boutle (:1982-2040)
-    const real zzrh0 = fmin(fmax(c.rprecrhmax + ((R(1.0) - c.rprecrhmax) * cs.zcovpmax) / fmax(zepsec, R(1.0) - za),
+    const real zzrh0 = fmin(fmax(c.rprecrhmax + cl_div(((R(1.0) - c.rprecrhmax) * cs.zcovpmax), fmax(zepsec, R(1.0) - za)),
                                  c.rprecrhmax), R(1.0));
     {
       const real zzrh = fmin(R(0.8), zzrh0);
       const real zqe = fmax(R(0.0), fmin(zqx[QV], zqsliq));
       if (zcovpclr > zepsec && zqxfg[QR] > zepsec && zqe < zzrh * zqsliq) { CLOUDSC_BRANCH_COUNT(16);
-        const real zpreclr = zqxfg[QR] / cs.zcovptot;
-        const real zfallcorr = cl_pow<real>(c.rdensref / zrho, R(0.4));
+        const real zpreclr = cl_div(zqxfg[QR], cs.zcovptot);
+        const real zfallcorr = cl_pow<real>(cl_div(c.rdensref, zrho), R(0.4));
         const real zesatliq = c.rv_rd * (c.r2es * e_liq);
-        const real zlambda = cl_pow<real>(c.rcl_fac1 / (zrho * zpreclr), c.rcl_fac2);
+        const real zlambda = cl_pow<real>(cl_div(c.rcl_fac1, (zrho * zpreclr)), c.rcl_fac2);
         const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * cl_pow<real>(ztp1, R(3.0))) * pap_k;
-        const real zcorr2 = (cl_pow<real>(ztp1 / R(273.0), R(1.5)) * R(393.0)) / (ztp1 + R(120.0));
+        const real zcorr2 = cl_div((cl_pow<real>(cl_div(ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
         const real zsubsat = fmax(zzrh * zqsliq - zqe, R(0.0));
-        const real zbeta = ((((R(0.5) / zqsliq) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (zcorr2 / zevap_denom) *
-                           (R(0.78) / cl_pow<real>(zlambda, c.rcl_const4r) + (c.rcl_const2r * sqrt(zrho * zfallcorr)) / (sqrt(zcorr2) * cl_pow<real>(zlambda, c.rcl_const3r)));
+        const real zbeta = ((((cl_div(R(0.5), zqsliq)) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (cl_div(zcorr2, zevap_denom)) *
+                           (cl_div(R(0.78), cl_pow<real>(zlambda, c.rcl_const4r)) + cl_div((c.rcl_const2r * sqrt(zrho * zfallcorr)), (sqrt(zcorr2) * cl_pow<real>(zlambda, c.rcl_const3r))));
         const real zdenom = R(1.0) + zbeta * c.ptsphy;
-        const real zdpevap = (((zcovpclr * zbeta) * c.ptsphy) * zsubsat) / zdenom;
+        const real zdpevap = cl_div((((zcovpclr * zbeta) * c.ptsphy) * zsubsat), zdenom);
         const real zevap = fmin(zdpevap, zqxfg[QR]);
         sa_rv = sa_rv + zevap;
-        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), ((cs.zcovptot - za) * zevap) / zqxfg[QR]));
+        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), cl_div(((cs.zcovptot - za) * zevap), zqxfg[QR])));
         zqxfg[QR] = zqxfg[QR] - zevap;
       }
     }
     // 4.5 evaporation of snow, Sundqvist (:2048-2087)
     {
       const real zzrh = zzrh0;
-      real zqe = (zqx[QV] - za * zqsice) / fmax(zepsec, R(1.0) - za);
+      real zqe = cl_div((zqx[QV] - za * zqsice), fmax(zepsec, R(1.0) - za));
       zqe = fmax(R(0.0), fmin(zqe, zqsice));
       if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) { CLOUDSC_BRANCH_COUNT(17);
         const real x = cs.zcovptot * zdtgdp;
-        const real zpreclr = (zqxfg[QS] * zcovpclr) / copysign(fmax(fabs(x), zepsilon), x);
-        const real zbeta1 = ((sqrt(pap_k / cc.paph_sfc) / c.rvrfactor) * zpreclr) / fmax(zcovpclr, zepsec);
+        const real zpreclr = cl_div((zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
+        const real zbeta1 = cl_div(((cl_div(sqrt(cl_div(pap_k, cc.paph_sfc)), c.rvrfactor)) * zpreclr), fmax(zcovpclr, zepsec));
         const real zbeta = c.rg_rpecons * cl_pow<real>(zbeta1, R(0.5777));
         const real zdenom = R(1.0) + (zbeta * c.ptsphy) * zcorqsice;
-        const real zdpr = ((((zcovpclr * zbeta) * (zqsice - zqe)) / zdenom) * zdp) * c.zrg_r;
+        const real zdpr = ((cl_div(((zcovpclr * zbeta) * (zqsice - zqe)), zdenom)) * zdp) * c.zrg_r;
         const real zdpevap = zdpr * zdtgdp;
         const real zevap = fmin(zdpevap, zqxfg[QS]);
         sa_sv = sa_sv + zevap;
-        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), ((cs.zcovptot - za) * zevap) / zqxfg[QS]));
+        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), cl_div(((cs.zcovptot - za) * zevap), zqxfg[QS])));
         zqxfg[QS] = zqxfg[QS] - zevap;
       }
     }
@@ -663,7 +663,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     if (zqxfg[QS] < c.rlmin) { sa_sv = sa_sv + zqxfg[QS]; }
 
     // 5.1 cloud cover (:2168-2180)
-    real zanew = (za + zsolac) / (R(1.0) + zsolab);
+    real zanew = cl_div((za + zsolac), (R(1.0) + zsolab));
     zanew = fmin(zanew, R(1.0));
     if (zanew < c.ramin) zanew = R(0.0);
     const real zda = zanew - zaorig;
@@ -679,7 +679,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       real z = R(0.0), psum, zrat;
       // m = ql: zsolqa[n][ql] = {ll, il, rl, sl, vl}
       psum = R(0.0) + sa_ll; psum = psum + (-sa_li); psum = psum + (-sa_lr); psum = psum + (-sa_ls); psum = psum + (-sa_lv);
-      { const real zmm = fmax(zqx[QL], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      { const real zmm = fmax(zqx[QL], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
       if (sa_ll < R(0.0)) { sa_ll = sa_ll * zrat; sa_ll = sa_ll * zrat; }
       if (-sa_li < R(0.0)) sa_li = sa_li * zrat;
       if (-sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
@@ -687,14 +687,14 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       if (-sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
       // m = qi: {li, ii, ri, si(0), vi}
       psum = R(0.0) + sa_li; psum = psum + sa_ii; psum = psum + (-sa_ir); psum = psum + z; psum = psum + (-sa_iv);
-      { const real zmm = fmax(zqx[QI], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      { const real zmm = fmax(zqx[QI], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
       if (sa_li < R(0.0)) sa_li = sa_li * zrat;
       if (sa_ii < R(0.0)) { sa_ii = sa_ii * zrat; sa_ii = sa_ii * zrat; }
       if (-sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
       if (-sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
       // m = qr: {lr, ir, rr, sr, vr}
       psum = R(0.0) + sa_lr; psum = psum + sa_ir; psum = psum + sa_rr; psum = psum + sa_sr; psum = psum + (-sa_rv);
-      { const real zmm = fmax(zqx[QR], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      { const real zmm = fmax(zqx[QR], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
       if (sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
       if (sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
       if (sa_rr < R(0.0)) { sa_rr = sa_rr * zrat; sa_rr = sa_rr * zrat; }
@@ -702,14 +702,14 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       if (-sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
       // m = qs: {ls, is(0), rs, ss, vs}
       psum = R(0.0) + sa_ls; psum = psum + z; psum = psum + (-sa_sr); psum = psum + sa_ss; psum = psum + (-sa_sv);
-      { const real zmm = fmax(zqx[QS], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      { const real zmm = fmax(zqx[QS], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
       if (sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
       if (-sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
       if (sa_ss < R(0.0)) { sa_ss = sa_ss * zrat; sa_ss = sa_ss * zrat; }
       if (-sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
       // m = qv: {lv, iv, rv, sv, vv(0)}
       psum = R(0.0) + sa_lv; psum = psum + sa_iv; psum = psum + sa_rv; psum = psum + sa_sv; psum = psum + z;
-      { const real zmm = fmax(zqx[QV], zepsec); zrat = zmm / fmax(R(0.0) - psum, zmm); }
+      { const real zmm = fmax(zqx[QV], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
       if (sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
       if (sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
       if (sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
@@ -745,17 +745,17 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       const real d_s = R(1.0) + fsink_s;
       // off-diagonals zqlhs[ql][qs] = -sb_ls, zqlhs[qi][qs] = -sb_is; LU scales row-wise by
       // the pivot of the eliminating column: zqlhs[n][m] /= zqlhs[n][n] for m > n.
-      const real u_ls = (-sb_ls) / d_l;    // zqlhs[ql][qs] after jn = ql
-      const real u_is = (-sb_is) / d_i;    // zqlhs[qi][qs] after jn = qi
+      const real u_ls = cl_div((-sb_ls), d_l);    // zqlhs[ql][qs] after jn = ql
+      const real u_is = cl_div((-sb_is), d_i);    // zqlhs[qi][qs] after jn = qi
       // forward substitution (step 1): zqxn[qs] -= zqlhs[ql][qs]*zqxn[ql] + zqlhs[qi][qs]*zqxn[qi]
       qn_s = qn_s - u_ls * qn_l;
       qn_s = qn_s - u_is * qn_i;
       // back substitution (step 2): vapour and the diagonal solves
-      qn_v = qn_v / R(1.0);
-      qn_s = qn_s / d_s;
-      qn_r = qn_r / d_r;
-      qn_i = qn_i / d_i;
-      qn_l = qn_l / d_l;
+      qn_v = cl_div(qn_v, R(1.0));
+      qn_s = cl_div(qn_s, d_s);
+      qn_r = cl_div(qn_r, d_r);
+      qn_i = cl_div(qn_i, d_i);
+      qn_l = cl_div(qn_l, d_l);
       // no small values (:2402-2412)
       if (qn_l < zepsec) { qn_v = qn_v + qn_l; qn_l = R(0.0); }
       if (qn_i < zepsec) { qn_v = qn_v + qn_i; qn_i = R(0.0); }

@@ -287,3 +287,32 @@ def test_kseg_full_size(lib, ds, kseg_env):
             assert np.array_equal(a[k], g.download(k)), k
     finally:
         g.close()
+
+
+# ---- branch coverage beyond the shipped state (same cases the oracle is pinned on) ----
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG])
+def test_random_perturbations_vs_oracle(lib, ds, oracle_mod, seed, variant):
+    import make_fixtures as mf
+    s = mf.perturbed(ds, seed)
+    out = run_gpu(s, 1000, 128, variant=variant)
+    ref = oracle_outputs(oracle_mod, s, 1000, 128)
+    assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "perturbed seed %d" % seed)
+
+
+@pytest.mark.parametrize("nssopt", [0, 2, 3])
+def test_nssopt_vs_oracle(lib, ds, oracle_mod, nssopt):
+    s = ds.copy()
+    s.params["nssopt"] = nssopt
+    out = run_gpu(s, 300, 128)
+    ref = oracle_outputs(oracle_mod, s, 300, 128)
+    assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "nssopt %d" % nssopt)
+
+
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
+def test_aerosol_flags_vs_oracle(lib, ds, oracle_mod, variant):
+    import make_fixtures as mf
+    s = mf.with_aerosols(ds)
+    out = run_gpu(s, 300, 128, variant=variant)
+    ref = oracle_outputs(oracle_mod, s, 300, 128)
+    assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "aerosol flags")

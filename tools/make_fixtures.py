@@ -97,6 +97,44 @@ def scenario(ds, name):
     return s
 
 
+
+def perturbed(ds, seed):
+    """Randomly perturbed copy of the state (temperature, humidity, condensate,
+    land mask, convection type, supersaturation) so that many branch
+    combinations are hit.  Used by the oracle-vs-reference tests and by the GPU
+    parity tests (same seed -> same inputs)."""
+    rng = np.random.default_rng(seed)
+    s = ds.copy()
+    klev, klon = s.klev, s.klon
+    s.inputs["pt"] = s.inputs["pt"] + rng.uniform(-5, 30, size=(1, klon)) + rng.normal(0, 1, size=(klev, klon))
+    s.inputs["pq"] = s.inputs["pq"] * rng.uniform(0.5, 1.8, size=(klev, klon))
+    pclv = s.inputs["pclv"].copy()
+    pclv[:4] += rng.uniform(0, 3e-5, size=(4, klev, klon)) * (rng.random((4, klev, klon)) < 0.3)
+    s.inputs["pclv"] = pclv
+    s.inputs["plsm"] = (rng.random(klon) < 0.5).astype(np.float64)
+    s.inputs["ktype"] = rng.integers(0, 3, size=klon).astype(np.int32)
+    s.inputs["psupsat"] = s.inputs["psupsat"] + rng.uniform(0, 1e-6, size=(klev, klon)) * (rng.random((klev, klon)) < 0.2)
+    s.reference = {}
+    return s
+
+
+def with_aerosols(ds, seed=11):
+    """Copy of the state with LAERICESED / LAERICEAUTO on and physically sized
+    aerosol inputs (the shipped PRE_ICE / PICRIT_AER / PNICE are all zero, which
+    makes the aerosol branches divide by zero): ice effective radius 10-100 um
+    (fall speed 0.002*re vs RVICE=0.13), critical ice content 1e-5..1e-4
+    (vs RLCRITSNOW=3e-5), ice number 0.01-0.1 (vs RNICE=0.027)."""
+    rng = np.random.default_rng(seed)
+    s = ds.copy()
+    shp = s.inputs["pt"].shape
+    s.inputs["pre_ice"] = rng.uniform(10.0, 100.0, size=shp)
+    s.inputs["picrit_aer"] = rng.uniform(1e-5, 1e-4, size=shp)
+    s.inputs["pnice"] = rng.uniform(0.01, 0.1, size=shp)
+    s.params["laericesed"] = 1
+    s.params["laericeauto"] = 1
+    s.reference = {}
+    return s
+
 def make_scenarios():
     import oracle  # the compiled reference kernel (oracle/_ref)
     if not oracle.ref_available():

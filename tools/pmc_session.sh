@@ -18,7 +18,7 @@ passes=(
 i=0
 for p in "${passes[@]}"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $p --kernel-trace --kernel-include-regex "kcache_entry|scc_entry" \
+  timeout -k 10 240 rocprofv3 --pmc $p --kernel-trace --kernel-include-regex "kcache_entry|scc_entry|kseg_entry" \
      -d $out/p$i -o run --output-format csv -- python3 $R/tools/prof_kernel.py "$@" > $out/p$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc: $p"

@@ -9,7 +9,7 @@ import sys
 from collections import defaultdict
 
 
-def load(dirname, kernel_regex="kcache_entry|scc_entry"):
+def load(dirname, kernel_regex="kcache_entry|scc_entry|kseg_entry"):
     import re
     vals = defaultdict(list)
     dur = []
