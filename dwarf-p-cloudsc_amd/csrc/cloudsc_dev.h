@@ -57,8 +57,19 @@ using cptr = const CLOUDSC_AS4 T*;
 // cache hit -- at no register cost.
 template <typename T>
 __device__ __forceinline__ cptr<T> launder_uniform(cptr<T> p) {
+#ifndef CLOUDSC_NO_LAUNDER
   asm volatile("" : "+s"(p));
+#endif
   return p;
+}
+// A parameter value materialised as a value (scalar register) at this point.
+// Without it, `cond ? c.a : c.b` and `x = c.a; if (flag) x = v;` are turned
+// into ONE load through a selected address -- a per-lane (vector, or flat via
+// a stack slot) load with a full memory wait inside the level loop.
+template <typename T>
+__device__ __forceinline__ T sval(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
 }
 template <typename T>
 __device__ __forceinline__ T launder_vgpr(T v) {

@@ -368,7 +368,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     }
 
     // 3.4 erosion of clouds by turbulent mixing (:1087-1118)
-    const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? c.zldifdt_conv : c.zldifdt0;
+    const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? sval(c.zldifdt_conv) : sval(c.zldifdt0);
     if (zli > zepsec) { CLOUDSC_BRANCH_COUNT(2);
       const real ze = zldifdt * fmax(zqsmix - zqx[QV], R(0.0));
       real zleros = za * ze;
@@ -505,7 +505,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       fsrc_r = cs.pfx_r * zdtgdp; sa_rr = sa_rr + fsrc_r; zqxfg[QR] = zqxfg[QR] + fsrc_r; zqpretot = zqpretot + zqxfg[QR];
       fsrc_s = cs.pfx_s * zdtgdp; sa_ss = sa_ss + fsrc_s; zqxfg[QS] = zqxfg[QS] + fsrc_s; zqpretot = zqpretot + zqxfg[QS];
     }
-    const real vqx_i = c.laericesed ? R(0.002) * in.pre_ice : c.rvice;
+    const real vqx_i = c.laericesed ? R(0.002) * in.pre_ice : sval(c.rvice);
     const real fsink_i = zdtgdp * (vqx_i * zrho);
     const real fsink_r = zdtgdp * (c.rvrain * zrho);
     const real fsink_s = zdtgdp * (c.rvsnow * zrho);
@@ -527,7 +527,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // 4.3a autoconversion to snow (:1616-1637)
     if (cold && zicecld > zepsec) { CLOUDSC_BRANCH_COUNT(9);
       real zzco = c.zzco_snow * cl_exp<real>(c.rsnowlin2 * (ztp1 - c.rtt));
-      real zlcrit = c.rlcritsnow;
+      real zlcrit = sval(c.rlcritsnow);
       if (c.laericeauto) {
         zlcrit = in.picrit_aer;
         zzco = zzco * cl_pow<real>(cl_div(c.rnice, in.pnice), R(0.333));
@@ -841,8 +841,8 @@ __device__ __forceinline__ ColConst<real> column_constants(const P& c, const KAr
   cc.ktype = ldg(A.ktype, u1, lo * (unsigned)(sizeof(int)) / (unsigned)sizeof(real));
   cc.paph_sfc = ldg(A.paph, uh + (size_t)A.klev * A.nproma, lo);
   const bool land = plsm > R(0.5);
-  cc.kk_const = land ? c.rcl_kk_cloud_num_land : c.rcl_kk_cloud_num_sea;
-  cc.kk_lcrit = land ? c.rclcrit_land : c.rclcrit_sea;
+  cc.kk_const = land ? sval(c.rcl_kk_cloud_num_land) : sval(c.rcl_kk_cloud_num_sea);
+  cc.kk_lcrit = land ? sval(c.rclcrit_land) : sval(c.rclcrit_sea);
   cc.kk_pow = cl_pow<real>(cc.kk_const, c.rcl_kkbaun);   // loop-invariant factor of the KK autoconversion (:1721)
   return cc;
 }
