@@ -88,14 +88,24 @@ __device__ __forceinline__ T launder_vgpr(T v) {
 __device__ __attribute__((noinline)) double cl_pow_ool(double x, double y);
 __device__ __attribute__((noinline)) float cl_pow_ool(float x, float y);
 #endif
+// pow is only ever applied to non-negative bases here (densities, ratios of
+// positive quantities, temperatures, slope parameters), where OCML's powr (the
+// x >= 0 power: no negative-base / integer-exponent handling) is the same
+// core computation as pow without the special-case fix-ups.
+extern "C" __device__ double __ocml_powr_f64(double, double);
+extern "C" __device__ float __ocml_powr_f32(float, float);
+__device__ __forceinline__ double cl_powr(double x, double y) { return __ocml_powr_f64(x, y); }
+__device__ __forceinline__ float cl_powr(float x, float y) { return __ocml_powr_f32(x, y); }
 template <typename real>
 __device__ __forceinline__ real cl_pow(real x, real y) {
 #if defined(CLOUDSC_ABLATE_POW)
   return x * y;
 #elif defined(CLOUDSC_NOINLINE_POW)
   return cl_pow_ool(x, y);
-#else
+#elif defined(CLOUDSC_LIBM_POW)
   return pow(x, y);
+#else
+  return cl_powr(x, y);
 #endif
 }
 template <typename real>

@@ -532,7 +532,7 @@ int expand_into(cloudsc_gpu_state* s, void* dst, const void* host_src, int nlev,
     e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   }
-  hipFree(d_src);
+  (void)hipFree(d_src);
   if (e != hipSuccess) return hip_fail(e, "expand");
   return CLOUDSC_OK;
 }
@@ -663,7 +663,7 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     if (e != hipSuccess) rc = hip_fail(e, "hipEventElapsedTime");
     if (ms) ms[r] = t;
   }
-  for (auto& x : ev) hipEventDestroy(x);
+  for (auto& x : ev) (void)hipEventDestroy(x);
   if (rc == CLOUDSC_OK && variant == CLOUDSC_VARIANT_KSEG) {
     // a segment whose predecessor never arrived gives up after a bounded spin
     // and counts itself here: its results are invalid
@@ -742,20 +742,20 @@ int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* re
     }
     stats[id] = t;
   }
-  hipFree(part);
-  hipFree(dref);
+  (void)hipFree(part);
+  (void)hipFree(dref);
   if (e != hipSuccess) return hip_fail(e, "validate");
   return CLOUDSC_OK;
 }
 
 int cloudsc_state_destroy(cloudsc_gpu_state_t* s) {
   if (!s) return CLOUDSC_OK;
-  hipSetDevice(s->device);
-  if (s->stream) hipStreamSynchronize(s->stream);
-  for (void* p : s->allocs) hipFree(p);
-  if (s->ev0) hipEventDestroy(s->ev0);
-  if (s->ev1) hipEventDestroy(s->ev1);
-  if (s->stream) hipStreamDestroy(s->stream);
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (void* p : s->allocs) (void)hipFree(p);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return CLOUDSC_OK;
 }
