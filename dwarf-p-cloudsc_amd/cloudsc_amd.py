@@ -341,6 +341,10 @@ def gpu_lib(path: Optional[str] = None):
     lib.cloudsc_gpu_init.argtypes = [C.c_int, C.POINTER(Params)]
     lib.cloudsc_gpu_run.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.POINTER(Fields), C.c_void_p]
+    lib.cloudsc_host_pipeline_create.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int,
+                                                 C.c_int, C.c_int, C.c_int, C.POINTER(Fields)]
+    lib.cloudsc_host_pipeline_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
+    lib.cloudsc_host_pipeline_destroy.argtypes = [C.c_void_p]
     _lib = lib
     return lib
 
@@ -430,6 +434,51 @@ class GpuState:
     def close(self) -> None:
         if getattr(self, "h", None):
             self.lib.cloudsc_state_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HostPipeline:
+    """Host-buffer CLOUDSC step (cloudsc_host_pipeline_* of cloudsc_amd.h): the
+    block-layout arrays live in host memory (pinned in place) and every step
+    copies inputs in and outputs out, chunked and overlapped over streams."""
+
+    def __init__(self, ds: Dataset, ngptot: int, nproma: int = 128, precision: int = FP64, device: int = 0,
+                 chunk_blocks: int = 64, nstreams: int = 3, col_offset: int = 0):
+        self.lib = gpu_lib()
+        self.ds, self.ngptot, self.nproma, self.precision = ds, ngptot, nproma, precision
+        self._params = Params.from_dict(ds.params)
+        check(self.lib.cloudsc_gpu_init(device, C.byref(self._params)))
+        self.state = make_host_state(ds, ngptot, nproma, precision, col_offset)
+        self._plude0 = self.state.arrays["plude"].copy()
+        f = self.state.fields()
+        if not (ds.params.get("laericesed") or ds.params.get("laericeauto")):
+            for name in AEROSOL_FIELDS:            # not read by the kernel: not transferred
+                setattr(f, name, None)
+        self._fields = f
+        h = C.c_void_p()
+        check(self.lib.cloudsc_host_pipeline_create(C.byref(h), device, precision, ngptot, nproma, ds.klev,
+                                                    chunk_blocks, nstreams, C.byref(f)))
+        self.h = h
+
+    def run(self, variant: int = VARIANT_KCACHE) -> float:
+        """One step; plude is restored on the host first (INOUT).  Returns ms."""
+        np.copyto(self.state.arrays["plude"], self._plude0)
+        ms = C.c_double()
+        check(self.lib.cloudsc_host_pipeline_run(self.h, variant, C.byref(ms)))
+        return ms.value
+
+    def outputs(self) -> Dict[str, np.ndarray]:
+        return state_outputs_to_template(self.state.arrays, self.ngptot)
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.cloudsc_host_pipeline_destroy(self.h)
             self.h = None
 
     def __del__(self):

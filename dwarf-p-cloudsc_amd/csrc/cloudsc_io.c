@@ -11,6 +11,8 @@
 #include "cloudsc_io.h"
 
 #include <ctype.h>
+#include <float.h>
+#include <math.h>
 #include <dlfcn.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -506,4 +508,47 @@ void cloudsc_io_reference(const cloudsc_dataset_t *ds, cloudsc_reference_t *r) {
   r->klon = ds->klon;
   r->klev = ds->klev;
   for (int i = 0; i < CLOUDSC_NVALID; i++) r->field[i] = ds->ref[i];
+}
+
+/* ------------------------------------------------------------------------ */
+/* host block layout: expansion and statistics                               */
+/* ------------------------------------------------------------------------ */
+static int kind_nlev(int kind, int klev) {
+  return kind == 0 ? klev : kind == 1 ? klev + 1 : kind == 2 ? CLOUDSC_NCLV * klev : 1;
+}
+
+void cloudsc_io_expand(const void *src, int kind, int is_int, int klev, int klon, int ngptot, int nproma,
+                       long long col_offset, int elem_size, void *dst) {
+  const int nlev = kind_nlev(kind, klev);
+  const long long nb = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  for (long long b = 0; b < nb; b++)
+    for (int l = 0; l < nlev; l++)
+      for (int i = 0; i < nproma; i++) {
+        const long long g = col_offset + b * nproma + i;
+        const size_t s = (size_t)l * klon + (size_t)(g % klon);
+        const size_t d = ((size_t)b * nlev + l) * nproma + i;
+        if (is_int) ((int *)dst)[d] = ((const int *)src)[s];
+        else if (elem_size == 8) ((double *)dst)[d] = ((const double *)src)[s];
+        else ((float *)dst)[d] = (float)((const double *)src)[s];
+      }
+}
+
+void cloudsc_io_field_stats(const double *ref, int kind, int klev, int klon, const void *field, int elem_size,
+                            int ngptot, int nproma, long long col_offset, cloudsc_stats_t *st) {
+  const int nlev = kind_nlev(kind, klev);
+  const long long nb = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  double mn = DBL_MAX, mx = -DBL_MAX, me = 0.0, es = 0.0, rs = 0.0;
+  for (long long b = 0; b < nb; b++) {
+    const long long bsize = ngptot - b * nproma < nproma ? ngptot - b * nproma : nproma;
+    for (int l = 0; l < nlev; l++)
+      for (long long i = 0; i < bsize; i++) {
+        const long long g = col_offset + b * nproma + i;
+        const size_t d = ((size_t)b * nlev + l) * nproma + (size_t)i;
+        const double v = elem_size == 8 ? ((const double *)field)[d] : (double)((const float *)field)[d];
+        const double r = ref[(size_t)l * klon + (size_t)(g % klon)];
+        const double df = fabs(v - r);
+        mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, df); es += df; rs += fabs(r);
+      }
+  }
+  st->minval = mn; st->maxval = mx; st->maxerr = me; st->errsum = es; st->refsum = rs;
 }

@@ -82,6 +82,21 @@ void cloudsc_io_free(cloudsc_dataset_t *ds);
 void cloudsc_io_template(const cloudsc_dataset_t *ds, cloudsc_template_t *t);
 void cloudsc_io_reference(const cloudsc_dataset_t *ds, cloudsc_reference_t *r);
 
+/* Host-side block layout (for the host-buffer path): expand template array
+ * `src` of kind (0 level, 1 half level, 2 species, 3 surface) into dst
+ * [nblocks][..][nproma] with the global map g % klon, g = col_offset + b*nproma + i
+ * (load_state.c:69-184; lanes past ngptot are filled the same way, like the C
+ * reference).  elem_size 8 (double), 4 (float, rounded from double) or 4 with
+ * is_int (int copy). */
+void cloudsc_io_expand(const void *src, int kind, int is_int, int klev, int klon, int ngptot, int nproma,
+                       long long col_offset, int elem_size, void *dst);
+
+/* ERROR_PRINT statistics (validate_mod.F90:118-146, fabs) of a block-layout
+ * field (double or float, elem_size 8/4) against a KLON-column template
+ * reference, over the ngptot active lanes. */
+void cloudsc_io_field_stats(const double *ref, int kind, int klev, int klon, const void *field, int elem_size,
+                            int ngptot, int nproma, long long col_offset, cloudsc_stats_t *st);
+
 const char *cloudsc_io_last_error(void);
 
 #ifdef __cplusplus

@@ -48,6 +48,7 @@
 
 typedef struct {
   int numomp, ngptot, nproma, ngpus, precision, variant, reps, warmup;
+  int transfer, chunk_blocks, nstreams;
   double tol;
   int tol_given;
   const char *input_h5, *reference_h5, *data_dir, *write_h5_dir;
@@ -86,6 +87,10 @@ static void usage(const char *prog) {
           "  --data DIR            raw dataset directory (default $CLOUDSC_DATA or the\n"
           "                        repository's tests/golden/cloudsc100)\n"
           "  --tol X               relative L1 gate per field (default 1e-12 for fp64)\n"
+          "  --transfer            host-buffer path: block-layout arrays in host memory,\n"
+          "                        H2D -> kernel -> D2H per chunk, overlapped on streams\n"
+          "                        (TOTAL includes the transfers, like cloudsc_driver.cu)\n"
+          "  --chunk B --streams S chunk size in NPROMA blocks (64) and streams (3)\n"
           "  --write-h5 DIR        write DIR/input.h5 and DIR/reference.h5 of the loaded\n"
           "                        dataset and exit\n",
           prog);
@@ -96,6 +101,7 @@ static int parse(int argc, char **argv, options_t *o) {
   o->numomp = 1; o->ngptot = 100; o->nproma = 4;     /* dwarf_cloudsc.c:25-27 defaults */
   o->ngpus = 1; o->precision = CLOUDSC_FP64; o->variant = CLOUDSC_VARIANT_KSEG;
   o->reps = 1; o->warmup = 1; o->tol = 1e-12;
+  o->chunk_blocks = 64; o->nstreams = 3;
   int npos = 0;
   long pos[3] = {0, 0, 0};
   for (int i = 1; i < argc; i++) {
@@ -121,6 +127,9 @@ static int parse(int argc, char **argv, options_t *o) {
     else if (!strcmp(a, "--data")) { NEEDV(); o->data_dir = v; }
     else if (!strcmp(a, "--tol")) { NEEDV(); o->tol = atof(v); o->tol_given = 1; }
     else if (!strcmp(a, "--write-h5")) { NEEDV(); o->write_h5_dir = v; }
+    else if (!strcmp(a, "--transfer")) o->transfer = 1;
+    else if (!strcmp(a, "--chunk")) { NEEDV(); o->chunk_blocks = atoi(v); }
+    else if (!strcmp(a, "--streams")) { NEEDV(); o->nstreams = atoi(v); }
     else if (!strcmp(a, "-h") || !strcmp(a, "--help")) return -1;
     else if (a[0] == '-' && a[1] == '-') { fprintf(stderr, "unknown option %s\n", a); return -1; }
     else {
@@ -199,6 +208,114 @@ static double print_error(const char *name, int ndim, const cloudsc_stats_t *s, 
   return rel;
 }
 
+/* ---- host-buffer path (--transfer) ---- */
+/* cloudsc_io input index -> cloudsc_fields_t member index */
+static int input_field_index(int i) {
+  if (i < 16) return i;                 /* pt .. plu */
+  if (i == 16) return 27;               /* plude (INOUT) */
+  if (i < 23) return i - 1;             /* psnde .. psupsat */
+  return i - 1;                         /* aerosols 22..26 */
+}
+/* validated field id -> cloudsc_fields_t member index */
+static const int k_valid_field[CLOUDSC_NVALID] = {27, 32, 33, 34, 35, 37, 36, 38, 39, 40, 41,
+                                                  42, 43, 44, 45, 46, 47, 30, 29, 28, 31};
+/* kinds of the outputs 28..47 */
+static const int k_out_kind[20] = {0, 0, 0, 2, 0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+
+static double print_error(const char *name, int ndim, const cloudsc_stats_t *s, int ngptot);
+
+static int run_transfer(const options_t *o, const cloudsc_dataset_t *ds) {
+  const int es = o->precision == CLOUDSC_FP64 ? 8 : 4;
+  const int nb = o->ngptot / o->nproma + (o->ngptot % o->nproma ? 1 : 0);
+  const int aer = ds->params.laericesed || ds->params.laericeauto;
+  cloudsc_fields_t f;
+  memset(&f, 0, sizeof(f));
+  void **fp = (void **)&f;
+  size_t host_bytes = 0;
+  double *plude0 = NULL;
+  int rc = CLOUDSC_OK;
+  /* inputs: expanded on the host (load_state.c) */
+  for (int i = 0; i < CLOUDSC_IO_NIN && !rc; i++) {
+    const int kind = cloudsc_io_input_kind[i];
+    const void *src = i == CLOUDSC_IO_KTYPE ? (const void *)ds->ktype : (const void *)ds->in[i];
+    if (!src || (i >= CLOUDSC_IO_FIRST_AEROSOL && !aer)) continue;
+    const int is_int = i == CLOUDSC_IO_KTYPE;
+    const size_t n = (size_t)nb * (size_t)(cloudsc_io_elems(kind, ds->klev, o->nproma));
+    const size_t bytes = n * (is_int ? sizeof(int) : (size_t)es);
+    void *dst = aligned_alloc(4096, (bytes + 4095) & ~(size_t)4095);
+    if (!dst) { rc = CLOUDSC_ENOMEM; break; }
+    cloudsc_io_expand(src, kind, is_int, ds->klev, ds->klon, o->ngptot, o->nproma, 0, is_int ? 4 : es, dst);
+    fp[input_field_index(i)] = dst;
+    host_bytes += bytes;
+    if (i == 16) {
+      plude0 = (double *)malloc(bytes);
+      if (!plude0) { rc = CLOUDSC_ENOMEM; break; }
+      memcpy(plude0, dst, bytes);
+    }
+  }
+  for (int j = 0; j < 20 && !rc; j++) {
+    const size_t bytes = (size_t)nb * (size_t)cloudsc_io_elems(k_out_kind[j], ds->klev, o->nproma) * es;
+    void *dst = aligned_alloc(4096, (bytes + 4095) & ~(size_t)4095);
+    if (!dst) { rc = CLOUDSC_ENOMEM; break; }
+    memset(dst, 0xff, bytes);            /* NaN: the callee must write every element */
+    fp[28 + j] = dst;
+    host_bytes += bytes;
+  }
+  const size_t plude_bytes = (size_t)nb * ds->klev * o->nproma * es;
+  cloudsc_host_pipeline_t *pipe = NULL;
+  if (!rc) rc = cloudsc_gpu_init(0, &ds->params);
+  if (!rc) rc = cloudsc_host_pipeline_create(&pipe, 0, o->precision, o->ngptot, o->nproma, ds->klev,
+                                             o->chunk_blocks, o->nstreams, &f);
+  double total_ms = 0.0;
+  for (int r = 0; r < o->warmup + o->reps && !rc; r++) {
+    memcpy(f.plude, plude0, plude_bytes);                 /* INOUT restored, outside the timing */
+    double ms = 0.0;
+    rc = cloudsc_host_pipeline_run(pipe, o->variant, &ms);
+    if (r >= o->warmup) total_ms += ms;
+  }
+  if (pipe) cloudsc_host_pipeline_destroy(pipe);
+  int bad = 0;
+  if (!rc) {
+    const double t = 1e-3 * total_ms;
+    const double cols = (double)o->ngptot * o->reps;
+    printf("     NUMOMP=%d, NGPTOT=%d, NPROMA=%d, NGPBLKS=%d\n", o->numomp, o->ngptot, o->nproma, nb);
+    printf(" Reference MFLOP count for 100 columns : %12.8f\n", 1.0e-06 * ZHPM);
+    printf(" %10s%10s%10s%10s%10s %4s : %10s%10s%10s\n", "NUMOMP", "NGPTOT", "#GP-cols", "#BLKS", "NPROMA",
+           "tid#", "Time(msec)", "MFlops/s", "col/s");
+    printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d TOTAL\n", o->numomp, o->ngptot, o->ngptot, nb, o->nproma, -1,
+           (int)(t * 1000.), (int)(1.0e-06 * ZHPM * (cols / 100.) / t), (int)(cols / t));
+    printf(" TIMING: steps=%d transfer_ms_per_step=%.4f columns_per_s=%.1f host_bytes=%zu chunk_blocks=%d "
+           "streams=%d (H2D + kernel + D2H, pinned host memory)\n",
+           o->reps, total_ms / o->reps, cols / t, host_bytes, o->chunk_blocks, o->nstreams);
+    if (ds->has_reference) {
+      printf(" %20s %s %20s %20s %20s %20s %20s\n", "Variable", "Dim", "MinValue", "MaxValue", "AbsMaxErr",
+             "AvgAbsErr/GP", "MaxRelErr-%");
+      const int gate = o->precision == CLOUDSC_FP64 || o->tol_given;
+      double worst = 0.0;
+      for (int v = 0; v < CLOUDSC_NVALID; v++) {
+        cloudsc_stats_t st;
+        const int kind = cloudsc_io_ref_kind[v];
+        cloudsc_io_field_stats(ds->ref[v], kind, ds->klev, ds->klon, fp[k_valid_field[v]], es, o->ngptot,
+                               o->nproma, 0, &st);
+        const double rel = print_error(cloudsc_io_print_names[v], kind == 3 ? 1 : kind == 2 ? 3 : 2, &st,
+                                       o->ngptot);
+        if (rel > worst) worst = rel;
+        if (gate && !(rel <= o->tol)) bad++;
+      }
+      if (gate)
+        printf(" VALIDATION: %s (worst relative L1 error %.3e, gate %.1e, %d field(s) over)\n",
+               bad ? "FAILED" : "PASSED", worst, o->tol, bad);
+      else
+        printf(" VALIDATION: reported only (fp32 vs the fp64 reference; worst relative L1 error %.3e)\n", worst);
+    }
+  } else {
+    fprintf(stderr, "dwarf-cloudsc-amd --transfer: %s (%s)\n", cloudsc_strerror(rc), cloudsc_last_hip_error());
+  }
+  for (int i = 0; i < 48; i++) free(fp[i]);
+  free(plude0);
+  return rc ? EXIT_FAILURE : (bad ? EXIT_FAILURE : EXIT_SUCCESS);
+}
+
 int main(int argc, char **argv) {
   options_t o;
   if (parse(argc, argv, &o)) { usage(argv[0]); return EXIT_FAILURE; }
@@ -249,6 +366,16 @@ int main(int argc, char **argv) {
     fprintf(stderr, "dwarf-cloudsc-amd: --gpus %d but only %d device(s)\n", o.ngpus, ndev);
     cloudsc_io_free(&ds);
     return EXIT_FAILURE;
+  }
+
+  if (o.transfer) {
+    printf(" CLOUDSC-AMD: %s, variant %s, host-buffer path (--transfer), 1 device; state: %s\n",
+           o.precision == CLOUDSC_FP64 ? "fp64" : "fp32",
+           o.variant == CLOUDSC_VARIANT_KSEG ? "kseg" : o.variant == CLOUDSC_VARIANT_KCACHE ? "kcache" : "scc",
+           ds.source);
+    rc = run_transfer(&o, &ds);
+    cloudsc_io_free(&ds);
+    return rc;
   }
 
   cloudsc_template_t tmpl;

@@ -239,6 +239,28 @@ long long cloudsc_state_field_elems(const cloudsc_gpu_state_t *state, int field_
 
 int cloudsc_state_destroy(cloudsc_gpu_state_t *state);
 
+/* ------------------------------------------------------------------------ */
+/* Host-buffer pipeline: the reference GPU drivers' H2D -> kernel -> D2H      */
+/* (cloudsc_driver.cu:344-456), chunked and overlapped across streams         */
+/* ------------------------------------------------------------------------ */
+typedef struct cloudsc_host_pipeline cloudsc_host_pipeline_t;
+
+/* `host` holds HOST pointers in block layout (full NPROMA blocks, the
+ * precision's element type, ktype int).  The arrays are pinned in place
+ * (hipHostRegister) until destroy; device buffers for `nstreams` chunks of
+ * `chunk_blocks` blocks are allocated here.  cloudsc_gpu_init must have been
+ * called for the device. */
+int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t **pipe, int device, int precision, int ngptot,
+                                 int nproma, int klev, int chunk_blocks, int nstreams,
+                                 const cloudsc_fields_t *host);
+
+/* One step over all columns: per chunk H2D(inputs, plude) -> kernel -> D2H
+ * (outputs, plude) on stream chunk % nstreams.  *ms = elapsed time of the
+ * whole pipeline (transfers included), HIP events on the null stream. */
+int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t *pipe, int variant, double *ms);
+
+int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t *pipe);
+
 #ifdef __cplusplus
 }
 #endif

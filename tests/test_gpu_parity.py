@@ -316,3 +316,33 @@ def test_aerosol_flags_vs_oracle(lib, ds, oracle_mod, variant):
     out = run_gpu(s, 300, 128, variant=variant)
     ref = oracle_outputs(oracle_mod, s, 300, 128)
     assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "aerosol flags")
+
+
+# ---- host-buffer pipeline (H2D -> kernel -> D2H, chunked over streams) ----
+@pytest.mark.parametrize("variant,chunk,nstreams", [(ca.VARIANT_KCACHE, 3, 2), (ca.VARIANT_KSEG, 2, 3),
+                                                     (ca.VARIANT_SCC, 5, 1), (ca.VARIANT_KCACHE, 100, 4)])
+def test_host_pipeline_equals_resident(lib, ds, variant, chunk, nstreams):
+    """Chunks of a few blocks (the last one partial, with the partial last
+    block) give the same bits as the device-resident run."""
+    ref = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KCACHE)
+    hp = ca.HostPipeline(ds, 1000, 128, chunk_blocks=chunk, nstreams=nstreams)
+    try:
+        hp.run(variant)
+        hp.run(variant)                     # plude restored between steps
+        out = hp.outputs()
+    finally:
+        hp.close()
+    for _, k in ca.VALIDATED:
+        assert np.array_equal(out[k], ref[k]), k
+
+
+def test_host_pipeline_fp32(lib, ds):
+    ref = run_gpu(ds, 1000, 128, precision=ca.FP32)
+    hp = ca.HostPipeline(ds, 1000, 128, precision=ca.FP32, chunk_blocks=4, nstreams=2)
+    try:
+        hp.run(ca.VARIANT_KCACHE)
+        out = hp.outputs()
+    finally:
+        hp.close()
+    for _, k in ca.VALIDATED:
+        assert np.array_equal(out[k], ref[k]), k

@@ -198,3 +198,35 @@ def test_cli_write_h5(tmp_path, io):
     r = subprocess.run([DWARF, "--write-h5", str(tmp_path)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "input.h5").exists() and (tmp_path / "reference.h5").exists()
+
+
+def test_host_expand_and_stats_match_python(io, ds):
+    """cloudsc_io_expand / cloudsc_io_field_stats (the host-buffer path of the
+    driver) == the numpy plumbing (ca.expand, ca.field_stats)."""
+    io.cloudsc_io_expand.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_longlong, C.c_int, C.c_void_p]
+    io.cloudsc_io_field_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                          C.c_int, C.c_longlong, C.POINTER(ca.Stats)]
+    kind_id = {"2d": 0, "2dh": 1, "3d": 2, "1d": 3}
+    ngptot, nproma, off = 1000, 128, 37
+    for name in ("pt", "paph", "pclv", "plsm", "ktype"):
+        src = np.ascontiguousarray(ds.inputs[name])
+        kind = ca.ALL_FIELDS[name]
+        is_int = name == "ktype"
+        for es, dt in ((8, np.float64), (4, np.float32)):
+            want = ca.expand(src, kind, ngptot, nproma, off, dtype=np.int32 if is_int else dt)
+            got = np.empty_like(want)
+            io.cloudsc_io_expand(src.ctypes.data, kind_id[kind], int(is_int), ds.klev, ds.klon, ngptot, nproma,
+                                 off, 4 if is_int else es, got.ctypes.data)
+            assert np.array_equal(got, want), (name, es)
+    for _, key in ca.VALIDATED[:6]:
+        ref = np.ascontiguousarray(ds.reference[key])
+        kind = ca.ALL_FIELDS[key]
+        fld = ca.expand(ref * (1 + 1e-9), kind, ngptot, nproma, 0)
+        st = ca.Stats()
+        io.cloudsc_io_field_stats(ref.ctypes.data, kind_id[kind], ds.klev, ds.klon, fld.ctypes.data, 8, ngptot,
+                                  nproma, 0, C.byref(st))
+        want = ca.field_stats(ca.blocks_to_columns(fld, ngptot), np.take(ref, np.arange(ngptot) % 100, axis=-1))
+        got = (st.minval, st.maxval, st.maxerr, st.errsum, st.refsum)
+        assert got[:3] == tuple(want[:3]), key
+        assert got[3] == pytest.approx(want[3], rel=1e-12) and got[4] == pytest.approx(want[4], rel=1e-12), key
