@@ -35,7 +35,9 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--ngptot", type=int, default=163840, help="columns per GPU")
-    p.add_argument("--nproma", type=int, default=128)
+    p.add_argument("--nproma", type=int, default=64,
+                   help="NPROMA (block = workgroup); 64 is the measured best for the persistent kernel "
+                        "(profiles/r01/nproma_sweep_all_variants.jsonl)")
     p.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
     p.add_argument("--variant", choices=["kseg", "kcache", "scc"], default="kseg")
     p.add_argument("--no-cpu-baseline", action="store_true")

@@ -10,6 +10,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace cloudsc {
 
 template <typename real>
@@ -133,10 +135,7 @@ __device__ __forceinline__ real cl_exp(real x) {
 // (tools/ab_compare.py: reference state, scenarios, random perturbations,
 // NSSOPT, aerosol flags, fp32, 163840 columns) confirms identical output bits.
 // CLOUDSC_IEEE_DIV restores the plain operator.
-template <typename real>
-__device__ __forceinline__ real cl_div(real n, real d);
-template <>
-__device__ __forceinline__ double cl_div<double>(double n, double d) {
+__device__ __forceinline__ double cl_div(double n, double d) {
 #ifdef CLOUDSC_IEEE_DIV
   return n / d;
 #else
@@ -150,8 +149,7 @@ __device__ __forceinline__ double cl_div<double>(double n, double d) {
   return __builtin_fma(rem, r, q);
 #endif
 }
-template <>
-__device__ __forceinline__ float cl_div<float>(float n, float d) {
+__device__ __forceinline__ float cl_div(float n, float d) {
 #ifdef CLOUDSC_IEEE_DIV
   return n / d;
 #else
@@ -164,6 +162,11 @@ __device__ __forceinline__ float cl_div<float>(float n, float d) {
   rem = __builtin_fmaf(-d, q, n);
   return __builtin_fmaf(rem, r, q);
 #endif
+}
+// explicit-precision form, cl_div<real>(a, b)
+template <typename real>
+__device__ __forceinline__ real cl_div(typename std::common_type<real>::type n, typename std::common_type<real>::type d) {
+  return cl_div(static_cast<real>(n), static_cast<real>(d));
 }
 
 // FOEALFA (src/common/include/fcttre.func.h; inlined at cloudsc_c.c:588,831,1162-1174)

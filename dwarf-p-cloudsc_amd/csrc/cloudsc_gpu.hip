@@ -155,16 +155,17 @@ template <> __device__ __forceinline__ cptr<DevParams<float>> dev_params<float>(
 // Kernel entry points.  The KArgs struct is the first explicit kernel argument,
 // i.e. it sits at offset 0 of the kernarg segment; the bodies read it (and the
 // parameter block) through constant-address-space pointers.
-template <typename real, int WAVES, int PF, bool AER>
+template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 __global__ void __launch_bounds__(256, WAVES) kcache_entry(const KArgs<real> a) {
   (void)a;
-  cloudsc_kcache_body<real, PF, AER>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), dev_params<real>());
+  cloudsc_kcache_body<real, PF, AER, LDSC>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
+                                           dev_params<real>());
 }
-template <typename real, int WAVES, int PF, bool AER>
+template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 __global__ void __launch_bounds__(256, WAVES) kseg_entry(const KArgs<real> a, const PersistArgs<real> pa) {
   (void)a;
-  cloudsc_kcache_persistent_body<real, PF, AER>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
-                                                dev_params<real>(), pa);
+  cloudsc_kcache_persistent_body<real, PF, AER, LDSC>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
+                                                      dev_params<real>(), pa);
 }
 template <typename real, bool AER>
 __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccScratch<real> s) {
@@ -227,8 +228,11 @@ __global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld
 namespace {
 
 template <typename real> int kcache_default_cfg();
-template <> int kcache_default_cfg<double>() { return 20; }
-template <> int kcache_default_cfg<float>() { return 31; }
+template <> int kcache_default_cfg<double>() { return 20; }    // 2 waves/SIMD, carried state in registers
+template <> int kcache_default_cfg<float>() { return 140; }   // 4 waves/SIMD, carried state in LDS
+template <typename real> int kseg_default_cfg();
+template <> int kseg_default_cfg<double>() { return 20; }
+template <> int kseg_default_cfg<float>() { return 31; }      // 3 waves/SIMD, register prefetch
 
 int validate_run_args(int device, int precision, int variant, int ngptot, int nproma, int klev) {
   int n = 0;
@@ -242,17 +246,22 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
   return CLOUDSC_OK;
 }
 
+// kernel configuration code: [1]<waves><pf> -- leading 1 = carried state in LDS
+#define CLOUDSC_FOR_EACH_CFG(X) \
+  X(10, 1, 0, false) X(11, 1, 1, false) X(20, 2, 0, false) X(21, 2, 1, false) X(30, 3, 0, false) \
+  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(130, 3, 0, true) \
+  X(131, 3, 1, true) X(140, 4, 0, true)
+
 template <typename real, bool AER>
 int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma, int cfg) {
   switch (cfg) {
-    case 10: hipLaunchKernelGGL((kcache_entry<real, 1, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
-    case 11: hipLaunchKernelGGL((kcache_entry<real, 1, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
-    case 20: hipLaunchKernelGGL((kcache_entry<real, 2, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
-    case 21: hipLaunchKernelGGL((kcache_entry<real, 2, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
-    case 30: hipLaunchKernelGGL((kcache_entry<real, 3, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
-    case 31: hipLaunchKernelGGL((kcache_entry<real, 3, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
-    case 40: hipLaunchKernelGGL((kcache_entry<real, 4, 0, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
-    case 41: hipLaunchKernelGGL((kcache_entry<real, 4, 1, AER>), dim3(nblocks), dim3(nproma), 0, st, a); break;
+#define X(code, w, pf, ldsc)                                                                                 \
+  case code:                                                                                                 \
+    hipLaunchKernelGGL((kcache_entry<real, w, pf, AER, ldsc>), dim3(nblocks), dim3(nproma),                  \
+                       ldsc ? carry_lds_bytes<real>(nproma) : 0, st, a);                                     \
+    break;
+    CLOUDSC_FOR_EACH_CFG(X)
+#undef X
     default: return CLOUDSC_EINVAL;
   }
   return CLOUDSC_OK;
@@ -286,16 +295,17 @@ void kseg_bounds(int nseg, int klev, int ncldtop, int* lev) {
   lev[nseg] = klev;
 }
 
-template <typename real, int WAVES, int PF, bool AER>
+template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
-  auto kern = kseg_entry<real, WAVES, PF, AER>;
+  auto kern = kseg_entry<real, WAVES, PF, AER, LDSC>;
+  const size_t lds = LDSC ? carry_lds_bytes<real>(nproma) : 0;
   // one workgroup per resident slot (an over-estimate only delays the extra
   // workgroups: progress never depends on residency, items are dequeued in order)
   static int cache[257] = {0};
   int& per_cu = cache[nproma];
   if (!per_cu) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, nproma, 0) != hipSuccess || n <= 0) n = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, nproma, lds) != hipSuccess || n <= 0) n = 1;
     per_cu = n;
   }
   int dev = 0, ncu = 0;
@@ -305,7 +315,7 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   int grid = per_cu * ncu;
   if (const char* e = getenv("CLOUDSC_KSEG_GRID")) grid = atoi(e) > 0 ? atoi(e) : grid;
   if (grid > nitems) grid = nitems;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(nproma), 0, st, a, pa);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(nproma), lds, st, a, pa);
   return CLOUDSC_OK;
 }
 
@@ -313,14 +323,10 @@ template <typename real, bool AER>
 int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
                 int cfg) {
   switch (cfg) {
-    case 10: return launch_kseg_cfg<real, 1, 0, AER>(st, a, pa, nproma, nitems);
-    case 11: return launch_kseg_cfg<real, 1, 1, AER>(st, a, pa, nproma, nitems);
-    case 20: return launch_kseg_cfg<real, 2, 0, AER>(st, a, pa, nproma, nitems);
-    case 21: return launch_kseg_cfg<real, 2, 1, AER>(st, a, pa, nproma, nitems);
-    case 30: return launch_kseg_cfg<real, 3, 0, AER>(st, a, pa, nproma, nitems);
-    case 31: return launch_kseg_cfg<real, 3, 1, AER>(st, a, pa, nproma, nitems);
-    case 40: return launch_kseg_cfg<real, 4, 0, AER>(st, a, pa, nproma, nitems);
-    case 41: return launch_kseg_cfg<real, 4, 1, AER>(st, a, pa, nproma, nitems);
+#define X(code, w, pf, ldsc) \
+  case code: return launch_kseg_cfg<real, w, pf, AER, ldsc>(st, a, pa, nproma, nitems);
+    CLOUDSC_FOR_EACH_CFG(X)
+#undef X
     default: return CLOUDSC_EINVAL;
   }
 }
@@ -342,7 +348,7 @@ int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, i
              : launch_kcache<real, false>(st, a, nblocks, nproma, cfg);
   } else if (variant == CLOUDSC_VARIANT_KSEG) {
     if (!scratch) return CLOUDSC_EINVAL;
-    int cfg = kcache_default_cfg<real>();
+    int cfg = kseg_default_cfg<real>();
     if (const char* e = getenv("CLOUDSC_KCACHE_CFG")) cfg = atoi(e);
     const int ncldtop = g_ncldtop[device];
     PersistArgs<real> pa;

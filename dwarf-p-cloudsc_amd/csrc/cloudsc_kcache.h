@@ -68,7 +68,7 @@ __device__ __forceinline__ T ldg(const T* ubase, size_t uidx, unsigned lane_byte
   return *(const T*)((const char*)(ubase + uidx) + lane_bytes);
 }
 template <typename T>
-__device__ __forceinline__ void stg(T* ubase, size_t uidx, unsigned lane_bytes, T v) {
+__device__ __forceinline__ void stg(T* ubase, size_t uidx, unsigned lane_bytes, typename std::common_type<T>::type v) {
   *(T*)((char*)(ubase + uidx) + lane_bytes) = v;
 }
 
@@ -103,6 +103,49 @@ struct CarryState {
   real pfx_i, pfx_r, pfx_s;             // zpfplsx[qi,qr,qs] arriving at level k
   real fl_lf, fl_if, fl_lng, fl_nng, fl_ltur, fl_itur;  // running flux sums (section 8)
 };
+
+// The same 19 values kept in LDS instead of registers: every wave owns 19
+// planes of 64 lanes ([wave][slot][lane], conflict-free, constant ds offsets).
+// They are touched a few times per level each, and taking them out of the
+// register file is what lets the fp64 kernel fit more waves per SIMD.
+// Accesses are volatile so that the compiler re-reads at each use instead of
+// keeping a register copy alive across the level.
+#define CLOUDSC_AS3 __attribute__((address_space(3)))
+template <typename real, int Q>
+struct LdsSlot {
+  CLOUDSC_AS3 real* base;               // this lane's slot 0
+  __device__ __forceinline__ operator real() const { return *(volatile CLOUDSC_AS3 real*)(base + Q * 64); }
+  __device__ __forceinline__ LdsSlot& operator=(real v) {
+    *(volatile CLOUDSC_AS3 real*)(base + Q * 64) = v;
+    return *this;
+  }
+  __device__ __forceinline__ LdsSlot& operator=(const LdsSlot& o) { return *this = (real)o; }
+};
+template <typename real>
+struct CarryLds {
+  static constexpr int kSlots = 19;
+  __device__ __forceinline__ explicit CarryLds(CLOUDSC_AS3 real* b)
+      : t_prev{b}, a_prev{b}, pap_prev{b}, zanewm1{b}, zcovptot{b}, zcovpmax{b}, zcldtopdist{b}, rainfrac{b},
+        qxnm1_l{b}, qxnm1_i{b}, pfx_i{b}, pfx_r{b}, pfx_s{b}, fl_lf{b}, fl_if{b}, fl_lng{b}, fl_nng{b},
+        fl_ltur{b}, fl_itur{b} {}
+  LdsSlot<real, 0> t_prev; LdsSlot<real, 1> a_prev; LdsSlot<real, 2> pap_prev; LdsSlot<real, 3> zanewm1;
+  LdsSlot<real, 4> zcovptot; LdsSlot<real, 5> zcovpmax; LdsSlot<real, 6> zcldtopdist; LdsSlot<real, 7> rainfrac;
+  LdsSlot<real, 8> qxnm1_l; LdsSlot<real, 9> qxnm1_i;
+  LdsSlot<real, 10> pfx_i; LdsSlot<real, 11> pfx_r; LdsSlot<real, 12> pfx_s;
+  LdsSlot<real, 13> fl_lf; LdsSlot<real, 14> fl_if; LdsSlot<real, 15> fl_lng; LdsSlot<real, 16> fl_nng;
+  LdsSlot<real, 17> fl_ltur; LdsSlot<real, 18> fl_itur;
+};
+// LDS bytes of the carried state for a workgroup of nproma lanes
+template <typename real>
+constexpr size_t carry_lds_bytes(int nproma) {
+  return (size_t)((nproma + 63) / 64) * CarryLds<real>::kSlots * 64 * sizeof(real);
+}
+template <typename real>
+__device__ __forceinline__ CLOUDSC_AS3 real* carry_lds_base() {
+  extern __shared__ __attribute__((aligned(16))) char cloudsc_dyn_lds[];
+  const int t = threadIdx.x;
+  return (CLOUDSC_AS3 real*)(CLOUDSC_AS3 char*)cloudsc_dyn_lds + (t >> 6) * (CarryLds<real>::kSlots * 64) + (t & 63);
+}
 
 // Result of section 1 at one level (the reference's level-sized temporaries).
 template <typename real>
@@ -197,11 +240,11 @@ __device__ __forceinline__ void init_level(const P& c, const LevelIn<real>& in, 
 }
 
 // ===== 3.-6. physics of one level ncldtop <= k (cloudsc_c.c:732-2508) =====
-template <typename real, typename P>
+template <typename real, typename P, typename CS>
 __device__ __forceinline__ void physics_level(const P& c, const int k, const int klev,
                                               const int ncldtop0, const LevelIn<real>& in,
                                               const Neighbors<real>& nb, const ColConst<real>& cc,
-                                              LevelState<real>& ls, CarryState<real>& cs, PhysOut<real>& po) {
+                                              LevelState<real>& ls, CS& cs, PhysOut<real>& po) {
   const real zepsilon = R(100.0) * (sizeof(real) == 8 ? (real)__DBL_EPSILON__ : (real)__FLT_EPSILON__);
   const real zepsec = R(1.0e-14);
   const real ztw1 = R(1329.31000000000), ztw2 = R(0.00746150000000000), ztw3 = R(85000.0000000000);
@@ -790,11 +833,11 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 }
 
 // ===== 8. flux diagnostics of one level (cloudsc_c.c:2521-2582), written at half level k+1 =====
-template <typename real, typename P>
+template <typename real, typename P, typename CS>
 __device__ __forceinline__ void flux_level(const P& c, const KArgs<real>& A, size_t h, unsigned lo,
                                            const LevelIn<real>& in, const LevelState<real>& ls,
                                            const PhysOut<real>& po, real paph_k, real paph_n,
-                                           CarryState<real>& cs) {
+                                           CS& cs) {
   const real zgdph_r = -c.zrg_r * (paph_n - paph_k) * c.zqtmst;
   const real lf = cs.fl_lf, fi = cs.fl_if, lng = cs.fl_lng, nng = cs.fl_nng;
   const real* zqxn = po.zqxn;
@@ -862,8 +905,8 @@ __device__ __forceinline__ void store_level(const KArgs<real>& A, size_t u2, siz
   stg(A.tlcld, u3 + ((size_t)4 * klev + k) * nproma, lo, R(0.0));
 }
 
-template <typename real>
-__device__ __forceinline__ void init_carry(CarryState<real>& cs) {
+template <typename real, typename CS>
+__device__ __forceinline__ void init_carry(CS& cs) {
   cs.t_prev = cs.a_prev = cs.pap_prev = R(0.0);
   cs.zanewm1 = cs.zcovptot = cs.zcovpmax = cs.zcldtopdist = cs.rainfrac = R(0.0);
   cs.qxnm1_l = cs.qxnm1_i = R(0.0);
@@ -881,9 +924,9 @@ __device__ __forceinline__ void init_carry(CarryState<real>& cs) {
 // kcache_levels runs levels [lev0, lev1) of block b for one (active) lane with
 // the carried state `cs`; the plain kernel runs [0, klev) in one go, the
 // persistent kernel (below) runs a column in level segments.
-template <typename real, int PF, bool AER>
+template <typename real, int PF, bool AER, typename CS>
 __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar, int b,
-                                              unsigned lo, int lev0, int lev1, CarryState<real>& cs) {
+                                              unsigned lo, int lev0, int lev1, CS& cs) {
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int nproma = A0.nproma, klev = A0.klev;
   const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
@@ -959,14 +1002,22 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
   }
 }
 
-template <typename real, int PF, bool AER>
+// carried state in registers (LDSC = false) or in LDS (LDSC = true)
+template <typename real>
+struct CarryRegs : CarryState<real> {
+  __device__ __forceinline__ explicit CarryRegs(CLOUDSC_AS3 real*) {}
+};
+template <typename real, bool LDSC>
+using CarryOf = typename std::conditional<LDSC, CarryLds<real>, CarryRegs<real>>::type;
+
+template <typename real, int PF, bool AER, bool LDSC>
 __device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar) {
   const KArgs<real>& A = *(const KArgs<real>*)ka;
   const int b = blockIdx.x, jl = threadIdx.x;
   if (jl >= A.nproma || b * A.nproma + jl >= A.ngptot) return;
   const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
-  CarryState<real> cs;
-  init_carry(cs);
+  CarryOf<real, LDSC> cs(carry_lds_base<real>());
+  init_carry<real>(cs);
   {
     CLOUDSC_PARAMS_HERE;
     flux_top(c, A, (size_t)b * (A.klev + 1) * A.nproma, lo);
@@ -1014,30 +1065,43 @@ __device__ __forceinline__ void stg_sc1(float* ubase, size_t uidx, unsigned lane
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename real>
-__device__ __forceinline__ void carry_io(real* st, size_t u, size_t plane, unsigned lo, CarryState<real>& cs,
-                                         bool save) {
-  real* f[kCarryN] = {&cs.t_prev, &cs.a_prev, &cs.pap_prev, &cs.zanewm1, &cs.zcovptot, &cs.zcovpmax,
-                      &cs.zcldtopdist, &cs.rainfrac, &cs.qxnm1_l, &cs.qxnm1_i, &cs.pfx_i, &cs.pfx_r, &cs.pfx_s,
-                      &cs.fl_lf, &cs.fl_if, &cs.fl_lng, &cs.fl_nng, &cs.fl_ltur, &cs.fl_itur};
-#pragma unroll
-  for (int q = 0; q < kCarryN; q++) {
-    if (save) stg_sc1(st, u + (size_t)q * plane, lo, *f[q]);
-    else *f[q] = ldg((const real*)st, u + (size_t)q * plane, lo);
-  }
+template <typename real, typename CS>
+__device__ __forceinline__ void carry_io(real* st, size_t u, size_t plane, unsigned lo, CS& cs, bool save) {
+#define CLOUDSC_CARRY_IO(q, m)                                                  \
+  if (save) stg_sc1(st, u + (size_t)(q) * plane, lo, (real)cs.m);               \
+  else cs.m = ldg((const real*)st, u + (size_t)(q) * plane, lo);
+  CLOUDSC_CARRY_IO(0, t_prev) CLOUDSC_CARRY_IO(1, a_prev) CLOUDSC_CARRY_IO(2, pap_prev)
+  CLOUDSC_CARRY_IO(3, zanewm1) CLOUDSC_CARRY_IO(4, zcovptot) CLOUDSC_CARRY_IO(5, zcovpmax)
+  CLOUDSC_CARRY_IO(6, zcldtopdist) CLOUDSC_CARRY_IO(7, rainfrac) CLOUDSC_CARRY_IO(8, qxnm1_l)
+  CLOUDSC_CARRY_IO(9, qxnm1_i) CLOUDSC_CARRY_IO(10, pfx_i) CLOUDSC_CARRY_IO(11, pfx_r)
+  CLOUDSC_CARRY_IO(12, pfx_s) CLOUDSC_CARRY_IO(13, fl_lf) CLOUDSC_CARRY_IO(14, fl_if)
+  CLOUDSC_CARRY_IO(15, fl_lng) CLOUDSC_CARRY_IO(16, fl_nng) CLOUDSC_CARRY_IO(17, fl_ltur)
+  CLOUDSC_CARRY_IO(18, fl_itur)
+#undef CLOUDSC_CARRY_IO
 }
 
-template <typename real, int PF, bool AER>
+template <typename real, int PF, bool AER, bool LDSC>
 __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar,
                                                                const PersistArgs<real>& P) {
   __shared__ int s_item;
   const KArgs<real>& A = *(const KArgs<real>*)ka;
   const int nproma = A.nproma, jl = threadIdx.x;
   const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
+  // Every branch around a barrier is wave-uniform, and visibly so to the
+  // compiler (SGPR conditions): the first wave of the workgroup does the
+  // dequeue, the polling and the flag store with all of its lanes (same address,
+  // same value), never a lane-0-only region.  A divergent `if (lane == 0)`
+  // inside this loop gets restructured into nested exec-masked loops whose
+  // barriers no longer pair up across waves.
+  const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;
+  const unsigned one = jl == 0 ? 1u : 0u;           // lane 0 counts, the others add 0
   for (;;) {
-    if (jl == 0) s_item = (int)__hip_atomic_fetch_add(P.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave0) {
+      const unsigned old = __hip_atomic_fetch_add(P.counter, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_item = (int)__builtin_amdgcn_readfirstlane(old);   // lane 0's value: the ticket
+    }
     __syncthreads();
-    const int item = s_item;
+    const int item = __builtin_amdgcn_readfirstlane(s_item);
     __syncthreads();                                   // s_item is rewritten next iteration
     if (item >= P.nitems) break;
     const int seg = item / P.nblocks, b = item - seg * P.nblocks;
@@ -1046,20 +1110,26 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
 #endif
     const bool active = jl < nproma && b * nproma + jl < A.ngptot;
     const size_t ust = (size_t)b * kCarryN * nproma;
-    CarryState<real> cs;
+    CarryOf<real, LDSC> cs(carry_lds_base<real>());
     if (seg == 0) {
-      init_carry(cs);
+      init_carry<real>(cs);
       if (active) {
         CLOUDSC_PARAMS_HERE;
         flux_top(c, A, (size_t)b * (A.klev + 1) * nproma, lo);
       }
     } else {
-      // consumer: one relaxed poll, one agent acquire, wait, barrier, plain loads
-      if (jl == 0) {
-        unsigned spins = 0;
-        while (__hip_atomic_load(P.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)seg) {
+      // consumer: one relaxed poll (bounded, with s_sleep), one agent acquire,
+      // wait, barrier, plain loads
+      if (wave0) {
+        for (unsigned spins = 0;; spins++) {
+          const unsigned f = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(P.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          if (f >= (unsigned)seg) break;
+          if (spins > (1u << 24)) {                      // bounded: never hang
+            __hip_atomic_fetch_add(P.err, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
           __builtin_amdgcn_s_sleep(4);
-          if (++spins > (1u << 24)) { atomicAdd(P.err, 1u); break; }   // bounded: never hang
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
@@ -1069,13 +1139,12 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
     }
     if (active) kcache_levels<real, PF, AER>(ka, cpar, b, lo, P.lev[seg], P.lev[seg + 1], cs);
     if (seg + 1 < P.nseg) {
-      // producer (G16 R1): sc1 payload stores, every wave drains, barrier, one
-      // lane stores the flag with an agent atomic; no L2 write-back needed
+      // producer (G16 R1): sc1 payload stores, every wave drains, barrier, the
+      // flag stored with an agent atomic
       if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, true);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (jl == 0)
-        __hip_atomic_store(P.flags + b, (unsigned)(seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (wave0) __hip_atomic_store(P.flags + b, (unsigned)(seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (active) {
       stg(((const KArgs<real>*)launder_uniform(ka))->prainfrac, (size_t)b * nproma, lo, cs.rainfrac);
     }

@@ -100,7 +100,7 @@ __device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const Scc
   // ---- sweep 2: physics (all levels written; physics from NCLDTOP down) ----
   const ColConst<real> cc = column_constants(SCC_C, SCC_A, u1, uh, lo);
   CarryState<real> cs;
-  init_carry(cs);
+  init_carry<real>(cs);
 #pragma unroll
   for (int m = 0; m < 3; m++) stg(S.pfx, upfb + (size_t)m * pstride, lo, R(0.0));   // zpfplsx(:,1) = 0
   for (int k = 0; k < klev; k++) {
