@@ -2,19 +2,28 @@
 # Round profile on the GPU box: rocprofv3 kernel-trace stats of the default
 # bench command, then FETCH_SIZE / WRITE_SIZE passes (each its own run, --pmc
 # with --kernel-trace only) for the bench kernel -> gpurun_out/prof/.
-# usage: tools/profile_round.sh [variant] [precision]
-variant=${1:-kseg}; prec=${2:-fp64}
+# usage: tools/profile_round.sh [variant] [precision] [nproma]
+variant=${1:-kseg}; prec=${2:-fp64}; nproma=${3:-64}
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 out=$R/gpurun_out/prof
 mkdir -p $out
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/stats_${variant}_${prec} -o bench --output-format csv \
-  -- python3 $R/bench.py --steps 20 --warmup 3 --variant $variant --precision $prec \
-  > $out/bench_under_rocprof_${variant}_${prec}.log 2>&1 || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d $out/pmc_${c}_${variant}_${prec} -o run --output-format csv \
-    -- python3 $R/tools/prof_kernel.py --variant $variant --precision $prec --reps 3 \
+    -- python3 $R/tools/prof_kernel.py --variant $variant --precision $prec --nproma $nproma --reps 3 \
     > $out/pmc_${c}_${variant}_${prec}.log 2>&1 || exit $?
 done
-python3 $R/tools/pmc_traffic.py ${variant}_${prec}_163840_128 $out/pmc_FETCH_SIZE_${variant}_${prec} \
+python3 $R/tools/pmc_traffic.py ${variant}_${prec}_163840_${nproma} $out/pmc_FETCH_SIZE_${variant}_${prec} \
   $out/pmc_WRITE_SIZE_${variant}_${prec} $out/traffic.json
+# the bench line reads its roofline.traffic from profiles/traffic_latest.json
+python3 - <<PY
+import json, os
+src, dst = "$out/traffic.json", "$R/profiles/traffic_latest.json"
+d = json.load(open(dst)) if os.path.exists(dst) else {}
+d.update(json.load(open(src)))
+json.dump(d, open(dst, "w"), indent=1, sort_keys=True)
+PY
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/stats_${variant}_${prec} -o bench --output-format csv \
+  -- python3 $R/bench.py --steps 20 --warmup 3 --variant $variant --precision $prec --nproma $nproma \
+  > $out/bench_under_rocprof_${variant}_${prec}.log 2>&1 || exit $?
+cp $R/profiles/traffic_latest.json $out/traffic_latest.json
