@@ -346,3 +346,68 @@ def test_host_pipeline_fp32(lib, ds):
         hp.close()
     for _, k in ca.VALIDATED:
         assert np.array_equal(out[k], ref[k]), k
+
+
+# ---- shapes beyond the reference's: other KLEV, tiny and ragged problems ----
+def sliced_levels(ds, lo_lev):
+    """The bottom KLEV-lo_lev levels of the state as a standalone column
+    (half-level pressures sliced to match)."""
+    s = ds.copy()
+    for name, kind in {**ca.INPUT_FIELDS, **ca.AEROSOL_FIELDS, **ca.INOUT_FIELDS}.items():
+        if name not in s.inputs:
+            continue
+        a = s.inputs[name]
+        if kind == "2d":
+            s.inputs[name] = np.ascontiguousarray(a[lo_lev:])
+        elif kind == "2dh":
+            s.inputs[name] = np.ascontiguousarray(a[lo_lev:])
+        elif kind == "3d":
+            s.inputs[name] = np.ascontiguousarray(a[:, lo_lev:])
+    s.klev = ds.klev - lo_lev
+    s.reference = {}
+    return s
+
+
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
+def test_other_klev_vs_oracle(lib, ds, oracle_mod, variant):
+    s = sliced_levels(ds, 77)                          # KLEV = 60
+    out = run_gpu(s, 300, 64, variant=variant)
+    ref = oracle_outputs(oracle_mod, s, 300, 64)
+    assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "klev 60")
+
+
+@pytest.mark.parametrize("ngptot,nproma", [(1, 1), (1, 64), (5, 256), (127, 64), (257, 256), (64, 32)])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG])
+def test_tiny_and_ragged(lib, ds, oracle_mod, ngptot, nproma, variant):
+    out = run_gpu(ds, ngptot, nproma, variant=variant)
+    ref = oracle_outputs(oracle_mod, ds, ngptot, nproma)
+    for _, k in ca.VALIDATED:
+        assert out[k].shape == ref[k].shape
+    assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "%d/%d" % (ngptot, nproma))
+
+
+def test_invalid_arguments(lib, ds):
+    import ctypes as C
+    g = ca.GpuState(ds, 256, 64)
+    try:
+        f = ca.Fields()
+        ca.check(lib.cloudsc_state_fields(g.h, C.byref(f)))
+        args = (0, None, ca.FP64)
+        assert lib.cloudsc_gpu_run(*args, 9, 256, 64, ds.klev, C.byref(f), None) == -1      # variant
+        assert lib.cloudsc_gpu_run(*args, ca.VARIANT_KCACHE, 0, 64, ds.klev, C.byref(f), None) == -1
+        assert lib.cloudsc_gpu_run(*args, ca.VARIANT_KCACHE, 256, 0, ds.klev, C.byref(f), None) == -1
+        assert lib.cloudsc_gpu_run(*args, ca.VARIANT_KCACHE, 256, 64, 1, C.byref(f), None) == -1
+        assert lib.cloudsc_gpu_run(*args, ca.VARIANT_KSEG, 256, 64, ds.klev, C.byref(f), None) == -1  # no ws
+        f.pt = None
+        assert lib.cloudsc_gpu_run(*args, ca.VARIANT_KCACHE, 256, 64, ds.klev, C.byref(f), None) == -1
+        assert lib.cloudsc_state_run(g.h, 7, 1, None) == -1
+        assert lib.cloudsc_state_run(g.h, ca.VARIANT_KCACHE, 0, None) == -1
+        assert lib.cloudsc_state_download(g.h, 21, None) == -1
+    finally:
+        g.close()
+    # parameters: NCLDTOP < 2 and NSSOPT out of range are rejected
+    for key, val in (("ncldtop", 1), ("nssopt", 4), ("ptsphy", 0.0)):
+        s = ds.copy()
+        s.params[key] = val
+        with pytest.raises(ca.CloudscError):
+            ca.GpuState(s, 64, 64)
