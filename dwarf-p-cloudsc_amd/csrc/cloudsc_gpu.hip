@@ -249,7 +249,7 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
 // kernel configuration code: [1]<waves><pf> -- leading 1 = carried state in LDS
 #define CLOUDSC_FOR_EACH_CFG(X) \
   X(10, 1, 0, false) X(11, 1, 1, false) X(20, 2, 0, false) X(21, 2, 1, false) X(30, 3, 0, false) \
-  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(130, 3, 0, true) \
+  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) X(130, 3, 0, true) \
   X(131, 3, 1, true) X(140, 4, 0, true)
 
 template <typename real, bool AER>
@@ -276,10 +276,11 @@ size_t kseg_scratch_bytes(int nblocks, int nproma) {
   return kseg_ctl_bytes(nblocks) + (size_t)nblocks * kCarryN * nproma * sizeof(real);
 }
 
-// measured (profiles/r01): fp64 2.72 ms one-shot -> 2.37 ms with 8 segments;
-// beyond 8 the tail no longer shrinks
-int kseg_nseg() {
-  int n = 8;
+// measured (profiles/r01/kseg_nseg_sweep*.jsonl): at NPROMA 128, 8 segments;
+// at NPROMA 64 (one wave per workgroup) 2-5 segments are within 1 %, more
+// cost hand-offs
+int kseg_nseg(int nproma) {
+  int n = nproma > 64 ? 8 : 4;
   if (const char* e = getenv("CLOUDSC_KSEG_NSEG")) n = atoi(e);
   return n < 1 ? 1 : (n > kMaxSeg ? kMaxSeg : n);
 }
@@ -356,7 +357,7 @@ int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, i
     pa.err = (unsigned*)scratch + 1;
     pa.flags = (unsigned*)((char*)scratch + 256);
     pa.state = (real*)((char*)scratch + kseg_ctl_bytes(nblocks));
-    pa.nseg = kseg_nseg();
+    pa.nseg = kseg_nseg(nproma);
     if (pa.nseg > klev) pa.nseg = klev;
     pa.nblocks = nblocks;
     pa.nitems = pa.nseg * nblocks;

@@ -1036,7 +1036,7 @@ __device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<D
 // The point: 2560 waves on 2048 wave slots leave the second round 75 % idle;
 // with NSEG segments the tail shrinks to a fraction of a segment.
 constexpr int kCarryN = 19;
-constexpr int kMaxSeg = 8;
+constexpr int kMaxSeg = 16;
 
 #ifdef CLOUDSC_KSEG_TRACE
 constexpr int kTraceMax = 1 << 16;

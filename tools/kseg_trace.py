@@ -19,7 +19,7 @@ lib = ca.gpu_lib()
 lib.cloudsc_kseg_trace.argtypes = [C.c_void_p, C.c_int]
 ds = ca.load_dataset()
 prec = ca.FP64 if (len(sys.argv) < 2 or sys.argv[1] == "fp64") else ca.FP32
-ngptot, nproma = 163840, 128
+ngptot, nproma = 163840, int(os.environ.get("TRACE_NPROMA", "64"))
 nb = ngptot // nproma
 g = ca.GpuState(ds, ngptot, nproma, prec)
 for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,3,4").split(",")]:
