@@ -73,7 +73,7 @@ def cpu_baseline(ds, ncols, nproma=32):
                           "src/cloudsc_c/cloudsc/cloudsc_c.c" if kind == "reference" else "oracle/cloudsc_oracle.c")}
 
 
-def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=64, nstreams=3):
+def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=32, nstreams=4):
     """Host-resident block-layout arrays (pinned in place), per chunk H2D ->
     kernel -> D2H overlapped on streams: the reference GPU drivers' TOTAL
     semantics (cloudsc_driver.cu:344-456).  plude is restored on the host

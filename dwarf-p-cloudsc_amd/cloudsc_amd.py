@@ -449,7 +449,7 @@ class HostPipeline:
     copies inputs in and outputs out, chunked and overlapped over streams."""
 
     def __init__(self, ds: Dataset, ngptot: int, nproma: int = 128, precision: int = FP64, device: int = 0,
-                 chunk_blocks: int = 64, nstreams: int = 3, col_offset: int = 0):
+                 chunk_blocks: int = 32, nstreams: int = 4, col_offset: int = 0):
         self.lib = gpu_lib()
         self.ds, self.ngptot, self.nproma, self.precision = ds, ngptot, nproma, precision
         self._params = Params.from_dict(ds.params)
