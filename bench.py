@@ -9,12 +9,13 @@ with NO data-path collective: rank r owns global columns
 a sharded run is bit-identical to an unsharded one).  torch.distributed (gloo)
 is used only for the barrier around the timed region and the max-over-ranks.
 
-A "step" = one CLOUDSC pass over the rank's NGPTOT resident columns: restore of
-the INOUT field plude (device copy, cloudsc_c.c:970,980) + one kernel launch.
-The timed region brackets exactly K steps with barrier + device sync on both
-sides; value = all columns of all ranks / max-over-ranks wall time.  The kernel
-alone is also timed with HIP events recorded on the launch stream
-(roofline.achieved uses that kernel time).
+A "step" = one CLOUDSC pass over the rank's NGPTOT resident columns: one
+kernel launch reading every input (plude from the state's pristine copy: the
+INOUT field is taken out of place, so repeated steps are the same step) and
+writing every output.  The timed region brackets exactly K steps with barrier
++ device sync on both sides; value = all columns of all ranks / max-over-ranks
+wall time.  The kernel alone is also timed with HIP events recorded on the
+launch stream (roofline.achieved uses that kernel time).
 """
 import argparse
 import json
@@ -115,7 +116,7 @@ def main():
     g.sync()
     ctl.barrier()
     t0 = time.perf_counter()
-    kernel_ms = g.run(variant, args.steps)      # plude restore + launch per step; events around launch
+    kernel_ms = g.run(variant, args.steps)      # one launch per step; events around each launch
     g.sync()
     t1 = time.perf_counter()
     ctl.barrier()

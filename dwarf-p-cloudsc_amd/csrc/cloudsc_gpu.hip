@@ -116,7 +116,7 @@ KArgs<real> make_args(const cloudsc_fields_t* f, int ngptot, int nproma, int kle
   a.pmfd = (const real*)f->pmfd; a.pa = (const real*)f->pa; a.pclv = (const real*)f->pclv;
   a.psupsat = (const real*)f->psupsat; a.picrit_aer = (const real*)f->picrit_aer;
   a.pre_ice = (const real*)f->pre_ice; a.pnice = (const real*)f->pnice;
-  a.plude = (real*)f->plude; a.tlt = (real*)f->tendency_loc_t; a.tlq = (real*)f->tendency_loc_q;
+  a.plude = (real*)f->plude; a.plude_in = (const real*)f->plude; a.tlt = (real*)f->tendency_loc_t; a.tlq = (real*)f->tendency_loc_q;
   a.tla = (real*)f->tendency_loc_a; a.tlcld = (real*)f->tendency_loc_cld;
   a.pcovptot = (real*)f->pcovptot; a.prainfrac = (real*)f->prainfrac_toprfz;
   a.pfsqlf = (real*)f->pfsqlf; a.pfsqif = (real*)f->pfsqif; a.pfcqnng = (real*)f->pfcqnng;
@@ -334,8 +334,9 @@ int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& p
 
 template <typename real>
 int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
-           void* scratch) {
-  const KArgs<real> a = make_args<real>(f, ngptot, nproma, klev);
+           void* scratch, const void* plude_in) {
+  KArgs<real> a = make_args<real>(f, ngptot, nproma, klev);
+  if (plude_in) a.plude_in = (const real*)plude_in;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
   const bool aer = g_aer[device];
   if (aer && (!f->pre_ice || !f->picrit_aer || !f->pnice)) return CLOUDSC_EINVAL;
@@ -424,15 +425,28 @@ long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int 
                                    : scc_scratch_bytes<float>(nblocks, nproma, klev);
 }
 
-int cloudsc_gpu_run(int device, void* stream, int precision, int variant, int ngptot, int nproma,
-                    int klev, const cloudsc_fields_t* f, void* scratch) {
+}  // extern "C"
+
+namespace {
+// plude_in: NULL = in place (the reference INOUT semantics); otherwise the
+// values of plude are read from there and the results written to f->plude
+int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
+                 const cloudsc_fields_t* f, void* scratch, const void* plude_in) {
   int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
   if (rc) return rc;
   if (!f || !fields_complete(f)) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
-  return precision == CLOUDSC_FP64 ? launch<double>(device, st, variant, f, ngptot, nproma, klev, scratch)
-                                   : launch<float>(device, st, variant, f, ngptot, nproma, klev, scratch);
+  return precision == CLOUDSC_FP64 ? launch<double>(device, st, variant, f, ngptot, nproma, klev, scratch, plude_in)
+                                   : launch<float>(device, st, variant, f, ngptot, nproma, klev, scratch, plude_in);
+}
+}  // namespace
+
+extern "C" {
+
+int cloudsc_gpu_run(int device, void* stream, int precision, int variant, int ngptot, int nproma,
+                    int klev, const cloudsc_fields_t* f, void* scratch) {
+  return gpu_run_impl(device, stream, precision, variant, ngptot, nproma, klev, f, scratch, nullptr);
 }
 
 const char* cloudsc_strerror(int code) {
@@ -655,11 +669,11 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   int rc = CLOUDSC_OK;
   for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
-    rc = cloudsc_state_reset(s);                                   // outside the event pair
-    if (rc) break;
+    // out of place: every step reads the pristine plude and writes the INOUT
+    // result to f.plude, so repeated steps see the same input with no restore copy
     HIPCHK(hipEventRecord(ev[2 * r], s->stream));
-    rc = cloudsc_gpu_run(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f,
-                         scratch);
+    rc = gpu_run_impl(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f, scratch,
+                      s->plude_pristine);
     HIPCHK(hipEventRecord(ev[2 * r + 1], s->stream));
   }
   hipError_t e = hipStreamSynchronize(s->stream);

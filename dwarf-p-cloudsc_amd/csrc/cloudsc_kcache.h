@@ -52,6 +52,7 @@ struct KArgs {
   const real *pap, *paph, *plsm;
   const int *ktype;
   const real *plu, *psnde, *pmfu, *pmfd, *pa, *pclv, *psupsat, *picrit_aer, *pre_ice, *pnice;
+  const real *plude_in;   // plude as read: == plude (in place, the C ABI) or a pristine copy (state runs)
   real *plude, *tlt, *tlq, *tla, *tlcld, *pcovptot, *prainfrac;
   real *pfsqlf, *pfsqif, *pfcqnng, *pfcqlng, *pfsqrf, *pfsqsf, *pfcqrng, *pfcqsng;
   real *pfsqltur, *pfsqitur, *pfplsl, *pfplsn, *pfhpsl, *pfhpsn;
@@ -170,7 +171,7 @@ __device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& 
   const size_t i = u2 + (size_t)k * nproma;
   L.pt = ldg(A.pt, i, lo); L.pq = ldg(A.pq, i, lo); L.ttt = ldg(A.ttt, i, lo); L.ttq = ldg(A.ttq, i, lo);
   L.tta = ldg(A.tta, i, lo); L.pa = ldg(A.pa, i, lo); L.pap = ldg(A.pap, i, lo);
-  L.plude = ldg((const real*)A.plude, i, lo); L.pvfl = ldg(A.pvfl, i, lo); L.pvfi = ldg(A.pvfi, i, lo);
+  L.plude = ldg(A.plude_in, i, lo); L.pvfl = ldg(A.pvfl, i, lo); L.pvfi = ldg(A.pvfi, i, lo);
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const size_t j = u3 + ((size_t)m * klev + k) * nproma;

@@ -213,13 +213,16 @@ int cloudsc_state_create(cloudsc_gpu_state_t **state, int device, int precision,
  * want to drive cloudsc_gpu_run themselves. */
 int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out);
 
-/* Restore plude from the pristine copy (outside any timed region). */
+/* Restore plude from the pristine copy -- for callers that run in place
+ * through cloudsc_gpu_run on the state's buffers. */
 int cloudsc_state_reset(cloudsc_gpu_state_t *state);
 
 /* Launch `reps` back-to-back steps of `variant` on the state's stream and
- * time each with HIP events recorded on that stream.  plude is restored
- * before every step by a device copy that is NOT inside the event pair.
- * ms_per_step[reps] receives the per-step kernel time (may be NULL). */
+ * time each with HIP events recorded on that stream.  The INOUT field plude
+ * is taken out of place: every step reads the pristine input copy and writes
+ * its result to the state's plude buffer, so repeated steps compute the same
+ * step without a restore copy.  ms_per_step[reps] receives the per-step
+ * kernel time (may be NULL). */
 int cloudsc_state_run(cloudsc_gpu_state_t *state, int variant, int reps, float *ms_per_step);
 
 /* Wait for all work of the state's stream. */
