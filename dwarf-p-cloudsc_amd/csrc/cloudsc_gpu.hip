@@ -276,23 +276,32 @@ size_t kseg_scratch_bytes(int nblocks, int nproma) {
   return kseg_ctl_bytes(nblocks) + (size_t)nblocks * kCarryN * nproma * sizeof(real);
 }
 
-// measured (profiles/r01/kseg_nseg_sweep*.jsonl): at NPROMA 128, 8 segments;
-// at NPROMA 64 (one wave per workgroup) 2-5 segments are within 1 %, more
-// cost hand-offs
+// Segmentation, measured (profiles/r01/kseg_nseg_sweep*.jsonl,
+// kseg_bounds_sweep_*.jsonl):
+//  - NPROMA > 64 (multi-wave workgroups, 1024 slots for 1280+ blocks): 8 even
+//    segments of the physics levels;
+//  - NPROMA <= 64 (one wave per workgroup, 2048 slots): 2 segments, the
+//    second one smaller ("guided": the items dequeued last are short, so the
+//    tail is short; lower levels also cost more per level) -- the split at
+//    NCLDTOP + 62 % of the physics levels; each hand-off costs 19 values out
+//    and in plus an L1 invalidate, so fewer segments win once the tail is short.
 int kseg_nseg(int nproma) {
-  int n = nproma > 64 ? 8 : 4;
+  int n = nproma > 64 ? 8 : 2;
   if (const char* e = getenv("CLOUDSC_KSEG_NSEG")) n = atoi(e);
   return n < 1 ? 1 : (n > kMaxSeg ? kMaxSeg : n);
 }
 
-// segment boundaries: levels above NCLDTOP only initialise and store (cheap),
-// so the physics levels are split evenly and the first segment also takes the
-// levels above the cloud top
-void kseg_bounds(int nseg, int klev, int ncldtop, int* lev) {
+void kseg_bounds(int nseg, int klev, int ncldtop, int nproma, int* lev) {
   const int top = ncldtop - 1 < klev ? (ncldtop - 1 > 0 ? ncldtop - 1 : 0) : klev;
   const int phys = klev - top;
   lev[0] = 0;
-  for (int sgm = 1; sgm < nseg; sgm++) lev[sgm] = top + (int)(((long long)phys * sgm + nseg / 2) / nseg);
+  if (nseg == 2 && nproma <= 64) {
+    lev[1] = top + (int)((62LL * phys + 50) / 100);
+    if (lev[1] <= 0) lev[1] = 1;
+    if (lev[1] >= klev) lev[1] = klev - 1;
+  } else {
+    for (int sgm = 1; sgm < nseg; sgm++) lev[sgm] = top + (int)(((long long)phys * sgm + nseg / 2) / nseg);
+  }
   lev[nseg] = klev;
 }
 
@@ -363,7 +372,20 @@ int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, i
     pa.nblocks = nblocks;
     pa.nitems = pa.nseg * nblocks;
     for (int q = 0; q <= kMaxSeg; q++) pa.lev[q] = klev;
-    kseg_bounds(pa.nseg, klev, ncldtop, pa.lev);
+    kseg_bounds(pa.nseg, klev, ncldtop, nproma, pa.lev);
+    if (const char* e = getenv("CLOUDSC_KSEG_BOUNDS")) {   // experiments: explicit interior boundaries
+      int n = 1, v = 0;
+      const char* q = e;
+      while (*q && n < kMaxSeg) {
+        v = (int)strtol(q, (char**)&q, 10);
+        if (v <= pa.lev[n - 1] || v >= klev) break;
+        pa.lev[n++] = v;
+        if (*q == ',') q++;
+      }
+      pa.nseg = n;
+      pa.lev[n] = klev;
+      pa.nitems = pa.nseg * nblocks;
+    }
     HIPCHK(hipMemsetAsync(scratch, 0, kseg_ctl_bytes(nblocks), st));
     rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, cfg)
              : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, cfg);

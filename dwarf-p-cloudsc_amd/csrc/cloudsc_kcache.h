@@ -928,6 +928,7 @@ __device__ __forceinline__ void init_carry(CS& cs) {
 template <typename real, int PF, bool AER, typename CS>
 __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar, int b,
                                               unsigned lo, int lev0, int lev1, CS& cs) {
+  if (lev0 >= lev1) return;                         // empty segment: no loads at lev0 (may be == klev)
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int nproma = A0.nproma, klev = A0.klev;
   const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
