@@ -40,7 +40,9 @@ def parse():
                    help="NPROMA (block = workgroup); 64 is the measured best for the persistent kernel "
                         "(profiles/r01/nproma_sweep_all_variants.jsonl)")
     p.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
-    p.add_argument("--variant", choices=["kseg", "kcache", "scc"], default="kseg")
+    p.add_argument("--variant", choices=["kseg", "kcache", "scc"], default=None,
+                   help="default: kseg for fp64 (2 waves/SIMD leave a tail the persistent kernel removes), "
+                        "kcache for fp32 (3-4 waves/SIMD, no tail)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--transfer", action="store_true",
                    help="also time the host-buffer path (H2D -> kernel -> D2H, chunked over streams): "
@@ -49,7 +51,10 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=65536, help="columns in the CPU baseline sample")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.variant is None:
+        a.variant = "kseg" if a.precision == "fp64" else "kcache"
+    return a
 
 
 def cpu_baseline(ds, ncols, nproma=32):
