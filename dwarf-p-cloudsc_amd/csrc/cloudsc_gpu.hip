@@ -14,6 +14,7 @@
 // the device is unavailable.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -310,13 +311,15 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   auto kern = kseg_entry<real, WAVES, PF, AER, LDSC>;
   const size_t lds = LDSC ? carry_lds_bytes<real>(nproma) : 0;
   // one workgroup per resident slot (an over-estimate only delays the extra
-  // workgroups: progress never depends on residency, items are dequeued in order)
-  static int cache[257] = {0};
-  int& per_cu = cache[nproma];
+  // workgroups: progress never depends on residency, items are dequeued in order).
+  // Cached per NPROMA; threads driving different devices may race here, hence atomics.
+  static std::atomic<int> cache[257];
+  int per_cu = cache[nproma].load(std::memory_order_relaxed);
   if (!per_cu) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, nproma, lds) != hipSuccess || n <= 0) n = 1;
     per_cu = n;
+    cache[nproma].store(n, std::memory_order_relaxed);
   }
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
