@@ -250,7 +250,7 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
 // kernel configuration code: [1]<waves><pf> -- leading 1 = carried state in LDS
 #define CLOUDSC_FOR_EACH_CFG(X) \
   X(10, 1, 0, false) X(11, 1, 1, false) X(20, 2, 0, false) X(21, 2, 1, false) X(30, 3, 0, false) \
-  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) X(130, 3, 0, true) \
+  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) X(122, 2, 2, true) X(130, 3, 0, true) X(132, 3, 2, true) X(22, 2, 2, false) \
   X(131, 3, 1, true) X(140, 4, 0, true)
 
 template <typename real, bool AER>

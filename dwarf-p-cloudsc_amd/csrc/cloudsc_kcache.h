@@ -929,6 +929,11 @@ template <typename real, int PF, bool AER, typename CS>
 __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar, int b,
                                               unsigned lo, int lev0, int lev1, CS& cs) {
   if (lev0 >= lev1) return;                         // empty segment: no loads at lev0 (may be == klev)
+  // PF: 0 = loads at the top of their level, 1 = level k+1 prefetched into
+  // registers, 2 = like 0, and the neighbour-level values (paph/pmfu/pmfd/plu of
+  // k, k+1) re-read every level instead of carried (fewer live registers,
+  // more L2 traffic)
+  constexpr bool PFX = PF == 1, NBR = PF == 2;
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int nproma = A0.nproma, klev = A0.klev;
   const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
@@ -953,7 +958,7 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
     nb.pmfu_n = ldg(A.pmfu, u2 + (size_t)l1 * nproma, lo);
     nb.pmfd_n = ldg(A.pmfd, u2 + (size_t)l1 * nproma, lo);
     nb.plu_n = ldg(A.plu, u2 + (size_t)l1 * nproma, lo);
-    if (PF) load_level<real, AER>(cur, A, u2, u3, lev0, klev, nproma, lo);
+    if (PFX) load_level<real, AER>(cur, A, u2, u3, lev0, klev, nproma, lo);
   }
 
   for (int kloop = lev0; kloop < lev1; kloop++) {
@@ -969,11 +974,20 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
       const int k1 = k + 1 < klev ? k + 1 : klev - 1;
       const int k2 = k + 2 < klev ? k + 2 : klev - 1;
       const int kh2 = k + 2 < klev + 1 ? k + 2 : klev;
-      if (!PF) load_level<real, AER>(cur, A, u2, u3, k, klev, nproma, lo);
-      if (PF) load_level<real, AER>(nxt, A, u2, u3, k1, klev, nproma, lo);
-      paph_nn = ldg(A.paph, uh + (size_t)kh2 * nproma, lo);
-      const size_t i2 = u2 + (size_t)k2 * nproma;
-      pmfu_nn = ldg(A.pmfu, i2, lo); pmfd_nn = ldg(A.pmfd, i2, lo); plu_nn = ldg(A.plu, i2, lo);
+      if (!PFX) load_level<real, AER>(cur, A, u2, u3, k, klev, nproma, lo);
+      if (PFX) load_level<real, AER>(nxt, A, u2, u3, k1, klev, nproma, lo);
+      if (NBR) {
+        nb.paph_k = ldg(A.paph, uh + (size_t)k * nproma, lo);
+        nb.paph_n = ldg(A.paph, uh + (size_t)(k + 1) * nproma, lo);
+        const size_t i0 = u2 + (size_t)k * nproma, i1 = u2 + (size_t)k1 * nproma;
+        nb.pmfu_k = ldg(A.pmfu, i0, lo); nb.pmfd_k = ldg(A.pmfd, i0, lo);
+        nb.pmfu_n = ldg(A.pmfu, i1, lo); nb.pmfd_n = ldg(A.pmfd, i1, lo); nb.plu_n = ldg(A.plu, i1, lo);
+        paph_nn = pmfu_nn = pmfd_nn = plu_nn = R(0.0);
+      } else {
+        paph_nn = ldg(A.paph, uh + (size_t)kh2 * nproma, lo);
+        const size_t i2 = u2 + (size_t)k2 * nproma;
+        pmfu_nn = ldg(A.pmfu, i2, lo); pmfd_nn = ldg(A.pmfd, i2, lo); plu_nn = ldg(A.plu, i2, lo);
+      }
     }
 
     LevelState<real> ls;
@@ -997,10 +1011,12 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
 
     // ---- rotate carried state ----
     cs.t_prev = ls.ztp1; cs.a_prev = ls.za; cs.pap_prev = cur.pap;
-    nb.paph_k = nb.paph_n; nb.paph_n = paph_nn;
-    nb.pmfu_k = nb.pmfu_n; nb.pmfd_k = nb.pmfd_n;
-    nb.pmfu_n = pmfu_nn; nb.pmfd_n = pmfd_nn; nb.plu_n = plu_nn;
-    if (PF) cur = nxt;
+    if (!NBR) {
+      nb.paph_k = nb.paph_n; nb.paph_n = paph_nn;
+      nb.pmfu_k = nb.pmfu_n; nb.pmfd_k = nb.pmfd_n;
+      nb.pmfu_n = pmfu_nn; nb.pmfd_n = pmfd_nn; nb.plu_n = plu_nn;
+    }
+    if (PFX) cur = nxt;
   }
 }
 
