@@ -1000,7 +1000,14 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
       po.plude_k = cur.plude;
       po.atend = R(0.0);
       po.zcovptot_out = R(0.0);
+#ifndef CLOUDSC_ABLATE_PHYSICS   // timing-only diagnostic build: the level loop without sections 3-6
       if (physics) physics_level(c, k, klev, ncldtop0, cur, nb, cc, ls, cs, po);
+#else                            // (every load kept alive, so the bytes moved are the same)
+      asm volatile("" :: "v"(cur.phrsw), "v"(cur.phrlw), "v"(cur.pvervel), "v"(cur.psnde), "v"(cur.psupsat),
+                   "v"(nb.pmfu_k), "v"(nb.pmfd_k), "v"(nb.plu_n), "v"(cc.kk_pow));
+      asm volatile("" :: "v"(cur.pclv[0]), "v"(cur.pclv[1]), "v"(cur.pclv[2]), "v"(cur.pclv[3]),
+                   "v"(cur.ttcld[0]), "v"(cur.ttcld[1]), "v"(cur.ttcld[2]), "v"(cur.ttcld[3]));
+#endif
     }
     {
       const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
@@ -1149,7 +1156,9 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
           }
           __builtin_amdgcn_s_sleep(4);
         }
+#ifndef CLOUDSC_KSEG_NO_ACQUIRE   // timing-only diagnostic build (unsynchronised: wrong in general)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
