@@ -1132,6 +1132,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
     const int seg = item / P.nblocks, b = item - seg * P.nblocks;
 #ifdef CLOUDSC_KSEG_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_ready = t_start;
 #endif
     const bool active = jl < nproma && b * nproma + jl < A.ngptot;
     const size_t ust = (size_t)b * kCarryN * nproma;
@@ -1162,6 +1163,9 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+#ifdef CLOUDSC_KSEG_TRACE
+      t_ready = __builtin_amdgcn_s_memrealtime();
+#endif
       if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, false);
     }
     if (active) kcache_levels<real, PF, AER>(ka, cpar, b, lo, P.lev[seg], P.lev[seg + 1], cs);
@@ -1180,8 +1184,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       g_kseg_trace[4 * item + 0] = t_start;
       g_kseg_trace[4 * item + 1] = __builtin_amdgcn_s_memrealtime();
       g_kseg_trace[4 * item + 2] = blockIdx.x;
-      g_kseg_trace[4 * item + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) * 65536ull +
-                                   __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+      g_kseg_trace[4 * item + 3] = t_ready;
     }
 #endif
   }

@@ -12,7 +12,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "dwarf-p-cloudsc_amd"))
-os.environ["CLOUDSC_AMD_LIB"] = os.path.join(REPO, "build", "libkseg_trace.so")
+os.environ.setdefault("CLOUDSC_AMD_LIB", os.path.join(REPO, "build", "libkseg_trace.so"))
 import cloudsc_amd as ca  # noqa: E402
 
 lib = ca.gpu_lib()
@@ -34,7 +34,7 @@ for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,3,4").spl
     st, en = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0   # microseconds
     dur = en - st
     wg = t[:, 2]
-    xcc = (t[:, 3] >> 16) & 0xF
+    wait = (t[:, 3] - t[:, 0]) / 100.0                       # microseconds spent polling for the predecessor
     makespan = en.max()
     busy = {}
     last_end = {}
@@ -51,6 +51,7 @@ for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,3,4").spl
            "seg_dur_us_mean": [round(float(d.mean()), 1) for d in segd],
            "seg_dur_us_p10_p90": [[round(float(np.percentile(d, 10)), 1), round(float(np.percentile(d, 90)), 1)]
                                   for d in segd],
-           "items_per_xcc": np.bincount(xcc, minlength=8).tolist()}
+           "wait_frac_of_busy": round(float(wait.sum() / dur.sum()), 4),
+           "seg_wait_us_mean": [round(float(wait[s * nb:(s + 1) * nb].mean()), 1) for s in range(nseg)]}
     print(json.dumps(out), flush=True)
 g.close()
