@@ -22,10 +22,12 @@
 
 #include "cloudsc_amd.h"
 #include "cloudsc_dev.h"
+#include "cloudsc_internal.h"
 #include "cloudsc_kcache.h"
 #include "cloudsc_scc.h"
 
 using namespace cloudsc;
+using namespace cloudsc_impl;
 
 // ---------------------------------------------------------------------------
 // __constant__ parameter mirrors
@@ -37,23 +39,20 @@ __device__ __attribute__((noinline)) float cloudsc::cl_pow_ool(float x, float y)
 __constant__ DevParams<double> g_params_dp;
 __constant__ DevParams<float> g_params_sp;
 
-namespace {
-
+namespace cloudsc_impl {
 thread_local char g_hip_err[256] = "";
-constexpr int kMaxDevices = 64;
-bool g_inited[kMaxDevices] = {false};
-bool g_aer[kMaxDevices] = {false};      // LAERICESED || LAERICEAUTO of the device's parameters
-int g_ncldtop[kMaxDevices] = {0};       // NCLDTOP of the device's parameters (KSEG segment bounds)
-
 int hip_fail(hipError_t e, const char* what) {
   snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s", what, hipGetErrorString(e));
   return CLOUDSC_EHIP;
 }
-#define HIPCHK(call)                                  \
-  do {                                                \
-    hipError_t e_ = (call);                           \
-    if (e_ != hipSuccess) return hip_fail(e_, #call); \
-  } while (0)
+void set_error_text(const char* text) { snprintf(g_hip_err, sizeof(g_hip_err), "%s", text); }
+}  // namespace cloudsc_impl
+
+namespace {
+
+bool g_inited[kMaxDevices] = {false};
+bool g_aer[kMaxDevices] = {false};      // LAERICESED || LAERICEAUTO of the device's parameters
+int g_ncldtop[kMaxDevices] = {0};       // NCLDTOP of the device's parameters (KSEG segment bounds)
 
 template <typename real>
 DevParams<real> fold_params(const cloudsc_params_t& p) {
@@ -129,6 +128,19 @@ KArgs<real> make_args(const cloudsc_fields_t* f, int ngptot, int nproma, int kle
   return a;
 }
 
+
+// the __constant__ mirror of a precision, as a constant-address-space pointer
+template <typename real> __device__ __forceinline__ cptr<DevParams<real>> dev_params();
+template <> __device__ __forceinline__ cptr<DevParams<double>> dev_params<double>() {
+  return (cptr<DevParams<double>>)&g_params_dp;
+}
+template <> __device__ __forceinline__ cptr<DevParams<float>> dev_params<float>() {
+  return (cptr<DevParams<float>>)&g_params_sp;
+}
+
+}  // namespace
+
+namespace cloudsc_impl {
 bool fields_complete(const cloudsc_fields_t* f) {
   const void* req[] = {f->pt, f->pq, f->tendency_tmp_t, f->tendency_tmp_q, f->tendency_tmp_a,
                        f->tendency_tmp_cld, f->pvfl, f->pvfi, f->phrsw, f->phrlw, f->pvervel, f->pap,
@@ -141,17 +153,7 @@ bool fields_complete(const cloudsc_fields_t* f) {
     if (!q) return false;
   return true;
 }
-
-// the __constant__ mirror of a precision, as a constant-address-space pointer
-template <typename real> __device__ __forceinline__ cptr<DevParams<real>> dev_params();
-template <> __device__ __forceinline__ cptr<DevParams<double>> dev_params<double>() {
-  return (cptr<DevParams<double>>)&g_params_dp;
-}
-template <> __device__ __forceinline__ cptr<DevParams<float>> dev_params<float>() {
-  return (cptr<DevParams<float>>)&g_params_sp;
-}
-
-}  // namespace
+}  // namespace cloudsc_impl
 
 // Kernel entry points.  The KArgs struct is the first explicit kernel argument,
 // i.e. it sits at offset 0 of the kernarg segment; the bodies read it (and the
@@ -175,55 +177,6 @@ __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccS
 }
 
 // ---------------------------------------------------------------------------
-// plumbing kernels: expansion and validation statistics
-// ---------------------------------------------------------------------------
-// dst[b][L][i] = src[L][(col_offset + b*nproma + i) % klon], L < nlev
-template <typename T, typename S>
-__global__ void expand_kernel(T* __restrict__ dst, const S* __restrict__ src, int nlev, int klon,
-                              int nproma, long long col_offset, long long nblocks) {
-  const long long b = blockIdx.y;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nlev * nproma; e += gridDim.x * blockDim.x) {
-    const int L = e / nproma, i = e - L * nproma;
-    const long long g = col_offset + b * nproma + i;
-    dst[(size_t)b * nlev * nproma + e] = (T)src[(size_t)L * klon + (size_t)(g % klon)];
-  }
-  (void)nblocks;
-}
-
-// One workgroup per NPROMA block: min/max of the field, max|d|, sum|d|, sum|ref|
-// over the active lanes of that block (validate_mod.F90:136-146, with fabs).
-template <typename real>
-__global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld, const double* __restrict__ ref,
-                                                    int nlev, int klon, int nproma, long long ngptot,
-                                                    long long col_offset, double* __restrict__ part) {
-  const long long b = blockIdx.x;
-  const long long bsize = (ngptot - b * nproma) < nproma ? (ngptot - b * nproma) : nproma;
-  double mn = __DBL_MAX__, mx = -__DBL_MAX__, me = 0.0, es = 0.0, rs = 0.0;
-  for (int e = threadIdx.x; e < nlev * nproma; e += blockDim.x) {
-    const int L = e / nproma, i = e - L * nproma;
-    if (i >= bsize) continue;
-    const long long g = col_offset + b * nproma + i;
-    const double v = (double)fld[(size_t)b * nlev * nproma + e];
-    const double r = ref[(size_t)L * klon + (size_t)(g % klon)];
-    const double d = fabs(v - r);
-    mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, d); es += d; rs += fabs(r);
-  }
-  __shared__ double s[5][256];
-  s[0][threadIdx.x] = mn; s[1][threadIdx.x] = mx; s[2][threadIdx.x] = me; s[3][threadIdx.x] = es; s[4][threadIdx.x] = rs;
-  __syncthreads();
-  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      const int t = threadIdx.x;
-      s[0][t] = fmin(s[0][t], s[0][t + w]); s[1][t] = fmax(s[1][t], s[1][t + w]);
-      s[2][t] = fmax(s[2][t], s[2][t + w]); s[3][t] += s[3][t + w]; s[4][t] += s[4][t + w];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0)
-    for (int q = 0; q < 5; q++) part[b * 5 + q] = s[q][0];
-}
-
-// ---------------------------------------------------------------------------
 // launch helpers
 // ---------------------------------------------------------------------------
 namespace {
@@ -235,17 +188,6 @@ template <typename real> int kseg_default_cfg();
 template <> int kseg_default_cfg<double>() { return 20; }
 template <> int kseg_default_cfg<float>() { return 31; }      // 3 waves/SIMD, register prefetch
 
-int validate_run_args(int device, int precision, int variant, int ngptot, int nproma, int klev) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CLOUDSC_ENODEV;
-  if (device < 0 || device >= n || device >= kMaxDevices) return CLOUDSC_ENODEV;
-  if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return CLOUDSC_EINVAL;
-  if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC && variant != CLOUDSC_VARIANT_KSEG)
-    return CLOUDSC_EINVAL;
-  if (ngptot <= 0 || nproma <= 0 || nproma > 256 || klev < 2) return CLOUDSC_EINVAL;
-  if (!g_inited[device]) return CLOUDSC_ENOINIT;
-  return CLOUDSC_OK;
-}
 
 // kernel configuration code: [1]<waves><pf> -- leading 1 = carried state in LDS
 #define CLOUDSC_FOR_EACH_CFG(X) \
@@ -452,7 +394,19 @@ long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int 
 
 }  // extern "C"
 
-namespace {
+namespace cloudsc_impl {
+int validate_run_args(int device, int precision, int variant, int ngptot, int nproma, int klev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CLOUDSC_ENODEV;
+  if (device < 0 || device >= n || device >= kMaxDevices) return CLOUDSC_ENODEV;
+  if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return CLOUDSC_EINVAL;
+  if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC && variant != CLOUDSC_VARIANT_KSEG)
+    return CLOUDSC_EINVAL;
+  if (ngptot <= 0 || nproma <= 0 || nproma > 256 || klev < 2) return CLOUDSC_EINVAL;
+  if (!g_inited[device]) return CLOUDSC_ENOINIT;
+  return CLOUDSC_OK;
+}
+
 // plude_in: NULL = in place (the reference INOUT semantics); otherwise the
 // values of plude are read from there and the results written to f->plude
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
@@ -465,7 +419,7 @@ int gpu_run_impl(int device, void* stream, int precision, int variant, int ngpto
   return precision == CLOUDSC_FP64 ? launch<double>(device, st, variant, f, ngptot, nproma, klev, scratch, plude_in)
                                    : launch<float>(device, st, variant, f, ngptot, nproma, klev, scratch, plude_in);
 }
-}  // namespace
+}  // namespace cloudsc_impl
 
 extern "C" {
 
@@ -511,495 +465,3 @@ long long cloudsc_abi_sizeof(int which) {
 
 }  // extern "C"
 
-// ---------------------------------------------------------------------------
-// C ABI: device-resident dwarf state
-// ---------------------------------------------------------------------------
-struct cloudsc_gpu_state {
-  int device, precision, ngptot, nproma, klev, klon, nblocks;
-  long long col_offset;
-  size_t es;                      // element size
-  hipStream_t stream;
-  hipEvent_t ev0, ev1;
-  cloudsc_fields_t f;             // device pointers
-  void* plude_pristine;
-  void* scratch;                  // SCC temporaries
-  void* kseg_ws;                  // KSEG counter, flags and carried state
-  std::vector<void*> allocs;
-};
-
-namespace {
-
-size_t field_elems(const cloudsc_gpu_state* s, int kind /*0 2d,1 2dh,2 3d,3 1d*/) {
-  const size_t nb = s->nblocks, np = s->nproma, kl = s->klev;
-  switch (kind) {
-    case 0: return nb * kl * np;
-    case 1: return nb * (kl + 1) * np;
-    case 2: return nb * 5 * kl * np;
-    default: return nb * np;
-  }
-}
-// validated field table: pointer slot and shape kind, in cloudsc_field_id order
-void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
-  const cloudsc_fields_t& f = s->f;
-  static const int kinds[CLOUDSC_NVALID] = {0, 0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 2};
-  void* const* slots[CLOUDSC_NVALID] = {
-      &f.plude, &f.pcovptot, &f.prainfrac_toprfz, &f.pfsqlf, &f.pfsqif, &f.pfcqlng, &f.pfcqnng,
-      &f.pfsqrf, &f.pfsqsf, &f.pfcqrng, &f.pfcqsng, &f.pfsqltur, &f.pfsqitur, &f.pfplsl, &f.pfplsn,
-      &f.pfhpsl, &f.pfhpsn, &f.tendency_loc_a, &f.tendency_loc_q, &f.tendency_loc_t, &f.tendency_loc_cld};
-  *kind = kinds[id];
-  return slots[id];
-}
-
-int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
-  hipError_t e = hipMalloc(p, bytes);
-  if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
-  s->allocs.push_back(*p);
-  return CLOUDSC_OK;
-}
-
-// upload one template array and expand it into the block-layout device field
-int expand_into(cloudsc_gpu_state* s, void* dst, const void* host_src, int nlev, bool is_int) {
-  const size_t src_bytes = (size_t)nlev * s->klon * (is_int ? sizeof(int) : sizeof(double));
-  void* d_src = nullptr;
-  HIPCHK(hipMalloc(&d_src, src_bytes));
-  hipError_t e = hipMemcpyAsync(d_src, host_src, src_bytes, hipMemcpyHostToDevice, s->stream);
-  if (e == hipSuccess) {
-    const int per = nlev * s->nproma;
-    dim3 grid((per + 255) / 256, s->nblocks);
-    if (is_int)
-      hipLaunchKernelGGL((expand_kernel<int, int>), grid, dim3(256), 0, s->stream, (int*)dst, (const int*)d_src,
-                         nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
-    else if (s->precision == CLOUDSC_FP64)
-      hipLaunchKernelGGL((expand_kernel<double, double>), grid, dim3(256), 0, s->stream, (double*)dst,
-                         (const double*)d_src, nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
-    else
-      hipLaunchKernelGGL((expand_kernel<float, double>), grid, dim3(256), 0, s->stream, (float*)dst,
-                         (const double*)d_src, nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
-  }
-  (void)hipFree(d_src);
-  if (e != hipSuccess) return hip_fail(e, "expand");
-  return CLOUDSC_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, int ngptot, int nproma,
-                         long long col_offset, const cloudsc_template_t* t, const cloudsc_params_t* params) {
-  if (!out || !t || !params || col_offset < 0) return CLOUDSC_EINVAL;
-  *out = nullptr;
-  int rc = cloudsc_gpu_init(device, params);
-  if (rc) return rc;
-  rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KCACHE, ngptot, nproma, t->klev);
-  if (rc) return rc;
-  if (t->klon <= 0) return CLOUDSC_EINVAL;
-  const void* req[] = {t->pt, t->pq, t->tendency_tmp_t, t->tendency_tmp_q, t->tendency_tmp_a,
-                       t->tendency_tmp_cld, t->pvfl, t->pvfi, t->phrsw, t->phrlw, t->pvervel, t->pap,
-                       t->paph, t->plsm, t->ktype, t->plu, t->plude, t->psnde, t->pmfu, t->pmfd, t->pa,
-                       t->pclv, t->psupsat};
-  for (const void* q : req)
-    if (!q) return CLOUDSC_EINVAL;
-  if (params->laericesed && !t->pre_ice) return CLOUDSC_EINVAL;
-  if (params->laericeauto && (!t->picrit_aer || !t->pnice)) return CLOUDSC_EINVAL;
-
-  cloudsc_gpu_state* s = new cloudsc_gpu_state();
-  s->device = device; s->precision = precision; s->ngptot = ngptot; s->nproma = nproma;
-  s->klev = t->klev; s->klon = t->klon; s->col_offset = col_offset;
-  s->nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
-  s->es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
-  std::memset(&s->f, 0, sizeof(s->f));
-  auto fail = [&](int r) { cloudsc_state_destroy(s); return r; };
-  if (hipSetDevice(device) != hipSuccess) return fail(CLOUDSC_ENODEV);
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
-  if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) return fail(CLOUDSC_EHIP);
-
-  const size_t n2 = field_elems(s, 0) * s->es, n2h = field_elems(s, 1) * s->es;
-  const size_t n3 = field_elems(s, 2) * s->es, n1 = field_elems(s, 3) * s->es;
-  const int kl = s->klev;
-  struct In { const void** dst; const void* src; int nlev; size_t bytes; bool is_int; };
-  cloudsc_fields_t& f = s->f;
-  void* plude_dev = nullptr;
-  In ins[] = {
-      {&f.pt, t->pt, kl, n2, false}, {&f.pq, t->pq, kl, n2, false},
-      {&f.tendency_tmp_t, t->tendency_tmp_t, kl, n2, false}, {&f.tendency_tmp_q, t->tendency_tmp_q, kl, n2, false},
-      {&f.tendency_tmp_a, t->tendency_tmp_a, kl, n2, false}, {&f.tendency_tmp_cld, t->tendency_tmp_cld, 5 * kl, n3, false},
-      {&f.pvfl, t->pvfl, kl, n2, false}, {&f.pvfi, t->pvfi, kl, n2, false}, {&f.phrsw, t->phrsw, kl, n2, false},
-      {&f.phrlw, t->phrlw, kl, n2, false}, {&f.pvervel, t->pvervel, kl, n2, false}, {&f.pap, t->pap, kl, n2, false},
-      {&f.paph, t->paph, kl + 1, n2h, false}, {&f.plsm, t->plsm, 1, n1, false},
-      {(const void**)&f.ktype, t->ktype, 1, (size_t)s->nblocks * nproma * sizeof(int), true},
-      {&f.plu, t->plu, kl, n2, false}, {&f.psnde, t->psnde, kl, n2, false}, {&f.pmfu, t->pmfu, kl, n2, false},
-      {&f.pmfd, t->pmfd, kl, n2, false}, {&f.pa, t->pa, kl, n2, false}, {&f.pclv, t->pclv, 5 * kl, n3, false},
-      {&f.psupsat, t->psupsat, kl, n2, false},
-      {&f.plcrit_aer, t->plcrit_aer, kl, n2, false}, {&f.picrit_aer, t->picrit_aer, kl, n2, false},
-      {&f.pre_ice, t->pre_ice, kl, n2, false}, {&f.pccn, t->pccn, kl, n2, false}, {&f.pnice, t->pnice, kl, n2, false},
-      {(const void**)&plude_dev, t->plude, kl, n2, false},
-  };
-  for (In& in : ins) {
-    if (!in.src) continue;
-    void* p = nullptr;
-    if ((rc = dalloc(s, &p, in.bytes))) return fail(rc);
-    if ((rc = expand_into(s, p, in.src, in.nlev, in.is_int))) return fail(rc);
-    *in.dst = p;
-  }
-  s->plude_pristine = plude_dev;
-  struct Out { void** dst; size_t bytes; };
-  Out outs[] = {{&f.plude, n2}, {&f.tendency_loc_t, n2}, {&f.tendency_loc_q, n2}, {&f.tendency_loc_a, n2},
-                {&f.tendency_loc_cld, n3}, {&f.pcovptot, n2}, {&f.prainfrac_toprfz, n1},
-                {&f.pfsqlf, n2h}, {&f.pfsqif, n2h}, {&f.pfcqnng, n2h}, {&f.pfcqlng, n2h}, {&f.pfsqrf, n2h},
-                {&f.pfsqsf, n2h}, {&f.pfcqrng, n2h}, {&f.pfcqsng, n2h}, {&f.pfsqltur, n2h}, {&f.pfsqitur, n2h},
-                {&f.pfplsl, n2h}, {&f.pfplsn, n2h}, {&f.pfhpsl, n2h}, {&f.pfhpsn, n2h}};
-  for (Out& o : outs) {
-    if ((rc = dalloc(s, o.dst, o.bytes))) return fail(rc);
-    if (hipMemsetAsync(*o.dst, 0xff, o.bytes, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);  // NaN
-  }
-  if (hipMemcpyAsync(f.plude, s->plude_pristine, n2, hipMemcpyDeviceToDevice, s->stream) != hipSuccess)
-    return fail(CLOUDSC_EHIP);
-  if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);
-  *out = s;
-  return CLOUDSC_OK;
-}
-
-int cloudsc_state_fields(const cloudsc_gpu_state_t* s, cloudsc_fields_t* out) {
-  if (!s || !out) return CLOUDSC_EINVAL;
-  *out = s->f;
-  return CLOUDSC_OK;
-}
-
-int cloudsc_state_reset(cloudsc_gpu_state_t* s) {
-  if (!s) return CLOUDSC_EINVAL;
-  HIPCHK(hipSetDevice(s->device));
-  HIPCHK(hipMemcpyAsync(s->f.plude, s->plude_pristine, field_elems(s, 0) * s->es, hipMemcpyDeviceToDevice,
-                        s->stream));
-  return CLOUDSC_OK;
-}
-
-int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) {
-  if (!s || reps <= 0) return CLOUDSC_EINVAL;
-  HIPCHK(hipSetDevice(s->device));
-  void* scratch = nullptr;
-  if (variant == CLOUDSC_VARIANT_SCC || variant == CLOUDSC_VARIANT_KSEG) {   // workspaces, allocated on first use
-    void*& ws = variant == CLOUDSC_VARIANT_SCC ? s->scratch : s->kseg_ws;
-    if (!ws) {
-      const long long nb = cloudsc_gpu_scratch_bytes(s->precision, variant, s->ngptot, s->nproma, s->klev);
-      if (nb <= 0) return CLOUDSC_EINVAL;
-      int rc0 = dalloc(s, &ws, (size_t)nb);
-      if (rc0) return rc0;
-    }
-    scratch = ws;
-  }
-  std::vector<hipEvent_t> ev(2 * (size_t)reps);
-  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
-  int rc = CLOUDSC_OK;
-  for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
-    // out of place: every step reads the pristine plude and writes the INOUT
-    // result to f.plude, so repeated steps see the same input with no restore copy
-    HIPCHK(hipEventRecord(ev[2 * r], s->stream));
-    rc = gpu_run_impl(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f, scratch,
-                      s->plude_pristine);
-    HIPCHK(hipEventRecord(ev[2 * r + 1], s->stream));
-  }
-  hipError_t e = hipStreamSynchronize(s->stream);
-  if (e != hipSuccess && rc == CLOUDSC_OK) rc = hip_fail(e, "hipStreamSynchronize");
-  for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
-    float t = 0.f;
-    e = hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]);
-    if (e != hipSuccess) rc = hip_fail(e, "hipEventElapsedTime");
-    if (ms) ms[r] = t;
-  }
-  for (auto& x : ev) (void)hipEventDestroy(x);
-  if (rc == CLOUDSC_OK && variant == CLOUDSC_VARIANT_KSEG) {
-    // a segment whose predecessor never arrived gives up after a bounded spin
-    // and counts itself here: its results are invalid
-    unsigned err = 0;
-    HIPCHK(hipMemcpy(&err, (unsigned*)scratch + 1, sizeof(err), hipMemcpyDeviceToHost));
-    if (err) {
-      std::snprintf(g_hip_err, sizeof(g_hip_err), "KSEG: %u segment hand-offs timed out", err);
-      rc = CLOUDSC_EHIP;
-    }
-  }
-  return rc;
-}
-
-int cloudsc_state_sync(cloudsc_gpu_state_t* s) {
-  if (!s) return CLOUDSC_EINVAL;
-  HIPCHK(hipSetDevice(s->device));
-  HIPCHK(hipStreamSynchronize(s->stream));
-  return CLOUDSC_OK;
-}
-
-long long cloudsc_state_field_elems(const cloudsc_gpu_state_t* s, int id) {
-  if (!s || id < 0 || id >= CLOUDSC_NVALID) return -1;
-  int kind;
-  valid_slot(s, id, &kind);
-  return (long long)field_elems(s, kind);
-}
-
-int cloudsc_state_download(cloudsc_gpu_state_t* s, int id, double* host) {
-  if (!s || !host || id < 0 || id >= CLOUDSC_NVALID) return CLOUDSC_EINVAL;
-  HIPCHK(hipSetDevice(s->device));
-  int kind;
-  void* const* slot = valid_slot(s, id, &kind);
-  const size_t n = field_elems(s, kind);
-  HIPCHK(hipStreamSynchronize(s->stream));
-  if (s->precision == CLOUDSC_FP64) {
-    HIPCHK(hipMemcpy(host, *slot, n * sizeof(double), hipMemcpyDeviceToHost));
-  } else {
-    std::vector<float> tmp(n);
-    HIPCHK(hipMemcpy(tmp.data(), *slot, n * sizeof(float), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < n; i++) host[i] = tmp[i];
-  }
-  return CLOUDSC_OK;
-}
-
-int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* ref, cloudsc_stats_t* stats) {
-  if (!s || !ref || !stats || ref->klon <= 0 || ref->klev != s->klev) return CLOUDSC_EINVAL;
-  HIPCHK(hipSetDevice(s->device));
-  HIPCHK(hipStreamSynchronize(s->stream));
-  double* part = nullptr;
-  double* dref = nullptr;
-  HIPCHK(hipMalloc(&part, (size_t)s->nblocks * 5 * sizeof(double)));
-  const size_t max_ref = (size_t)5 * (s->klev + 1) * ref->klon;
-  hipError_t e = hipMalloc(&dref, max_ref * sizeof(double));
-  std::vector<double> h((size_t)s->nblocks * 5);
-  for (int id = 0; id < CLOUDSC_NVALID && e == hipSuccess; id++) {
-    int kind;
-    void* const* slot = valid_slot(s, id, &kind);
-    const int nlev = kind == 0 ? s->klev : kind == 1 ? s->klev + 1 : kind == 2 ? 5 * s->klev : 1;
-    if (!ref->field[id]) { e = hipErrorInvalidValue; break; }
-    e = hipMemcpy(dref, ref->field[id], (size_t)nlev * ref->klon * sizeof(double), hipMemcpyHostToDevice);
-    if (e != hipSuccess) break;
-    if (s->precision == CLOUDSC_FP64)
-      hipLaunchKernelGGL(stats_kernel<double>, dim3(s->nblocks), dim3(256), 0, s->stream, (const double*)*slot,
-                         dref, nlev, ref->klon, s->nproma, (long long)s->ngptot, s->col_offset, part);
-    else
-      hipLaunchKernelGGL(stats_kernel<float>, dim3(s->nblocks), dim3(256), 0, s->stream, (const float*)*slot,
-                         dref, nlev, ref->klon, s->nproma, (long long)s->ngptot, s->col_offset, part);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
-    if (e == hipSuccess) e = hipMemcpy(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) break;
-    cloudsc_stats_t t = {__DBL_MAX__, -__DBL_MAX__, 0.0, 0.0, 0.0};
-    for (int b = 0; b < s->nblocks; b++) {            // block order: deterministic
-      t.minval = fmin(t.minval, h[b * 5 + 0]); t.maxval = fmax(t.maxval, h[b * 5 + 1]);
-      t.maxerr = fmax(t.maxerr, h[b * 5 + 2]); t.errsum += h[b * 5 + 3]; t.refsum += h[b * 5 + 4];
-    }
-    stats[id] = t;
-  }
-  (void)hipFree(part);
-  (void)hipFree(dref);
-  if (e != hipSuccess) return hip_fail(e, "validate");
-  return CLOUDSC_OK;
-}
-
-int cloudsc_state_destroy(cloudsc_gpu_state_t* s) {
-  if (!s) return CLOUDSC_OK;
-  (void)hipSetDevice(s->device);
-  if (s->stream) (void)hipStreamSynchronize(s->stream);
-  for (void* p : s->allocs) (void)hipFree(p);
-  if (s->ev0) (void)hipEventDestroy(s->ev0);
-  if (s->ev1) (void)hipEventDestroy(s->ev1);
-  if (s->stream) (void)hipStreamDestroy(s->stream);
-  delete s;
-  return CLOUDSC_OK;
-}
-
-}  // extern "C"
-
-// ---------------------------------------------------------------------------
-// C ABI: host-buffer pipeline
-// ---------------------------------------------------------------------------
-// The reference GPU drivers copy every block-layout host array to the device,
-// run, and copy the outputs back (cloudsc_driver.cu:344-456; the "field"
-// variant of README.md:311-330 overlaps them).  Here the blocks are cut into
-// chunks of `chunk_blocks` NPROMA blocks -- one contiguous range of every
-// field, because the layout is block-major -- and chunk c runs on stream
-// c % nstreams: H2D of its inputs, the kernel, D2H of its outputs.  The host
-// arrays are pinned in place (hipHostRegister) once, at creation.
-namespace {
-
-enum FieldKind { FK_LEVEL, FK_HALF, FK_SPECIES, FK_SURFACE };
-enum FieldDir { FD_IN, FD_INOUT, FD_OUT, FD_AEROSOL };
-struct FieldDesc { int kind, dir, is_int; };
-// cloudsc_fields_t member order (include/cloudsc_amd.h)
-constexpr FieldDesc kFieldTable[] = {
-    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_IN, 0},   {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_HALF, FD_IN, 0},    {FK_SURFACE, FD_IN, 0}, {FK_SURFACE, FD_IN, 1}, {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
-    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
-    {FK_LEVEL, FD_INOUT, 0},
-    {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_SPECIES, FD_OUT, 0},
-    {FK_LEVEL, FD_OUT, 0},  {FK_SURFACE, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0}};
-constexpr int kNumFields = (int)(sizeof(kFieldTable) / sizeof(kFieldTable[0]));
-static_assert(sizeof(cloudsc_fields_t) == kNumFields * sizeof(void*), "field table out of sync with the header");
-
-size_t per_block_elems(int kind, int nproma, int klev) {
-  switch (kind) {
-    case FK_LEVEL: return (size_t)klev * nproma;
-    case FK_HALF: return (size_t)(klev + 1) * nproma;
-    case FK_SPECIES: return (size_t)CLOUDSC_NCLV * klev * nproma;
-    default: return (size_t)nproma;
-  }
-}
-
-}  // namespace
-
-struct cloudsc_host_pipeline {
-  int device, precision, ngptot, nproma, klev, nblocks, chunk_blocks, nstreams;
-  size_t es;
-  cloudsc_fields_t host;
-  std::vector<void*> pinned;
-  struct Slot {
-    hipStream_t st = nullptr;
-    cloudsc_fields_t dev{};
-    void* scratch = nullptr;
-    size_t scratch_bytes = 0;
-    int scratch_variant = 0;
-  };
-  std::vector<Slot> slots;
-  std::vector<void*> allocs;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-};
-
-extern "C" {
-
-int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p);
-
-int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int precision, int ngptot, int nproma,
-                                 int klev, int chunk_blocks, int nstreams, const cloudsc_fields_t* host) {
-  if (!out || !host || chunk_blocks <= 0 || nstreams <= 0 || nstreams > 16) return CLOUDSC_EINVAL;
-  *out = nullptr;
-  int rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KCACHE, ngptot, nproma, klev);
-  if (rc) return rc;
-  if (!fields_complete(host)) return CLOUDSC_EINVAL;
-  cloudsc_host_pipeline* p = new cloudsc_host_pipeline();
-  p->device = device; p->precision = precision; p->ngptot = ngptot; p->nproma = nproma; p->klev = klev;
-  p->nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
-  p->chunk_blocks = chunk_blocks < p->nblocks ? chunk_blocks : p->nblocks;
-  p->nstreams = nstreams;
-  p->es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
-  p->host = *host;
-  auto fail = [&](int r) { cloudsc_host_pipeline_destroy(p); return r; };
-  if (hipSetDevice(device) != hipSuccess) return fail(CLOUDSC_ENODEV);
-  void* const* hf = (void* const*)&p->host;
-  // pin the caller's arrays in place (already-pinned memory is fine)
-  for (int i = 0; i < kNumFields; i++) {
-    if (!hf[i]) continue;
-    const FieldDesc& d = kFieldTable[i];
-    const size_t bytes = (size_t)p->nblocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : p->es);
-    hipError_t e = hipHostRegister(hf[i], bytes, hipHostRegisterDefault);
-    if (e == hipSuccess) p->pinned.push_back(hf[i]);
-    else if (e != hipErrorHostMemoryAlreadyRegistered) { hip_fail(e, "hipHostRegister"); return fail(CLOUDSC_EHIP); }
-    else (void)hipGetLastError();
-  }
-  p->slots.resize(nstreams);
-  for (auto& s : p->slots) {
-    if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
-    void** df = (void**)&s.dev;
-    for (int i = 0; i < kNumFields; i++) {
-      if (!hf[i]) continue;
-      const FieldDesc& d = kFieldTable[i];
-      const size_t bytes =
-          (size_t)p->chunk_blocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : p->es);
-      void* q = nullptr;
-      if (hipMalloc(&q, bytes) != hipSuccess) { hip_fail(hipErrorOutOfMemory, "hipMalloc"); return fail(CLOUDSC_ENOMEM); }
-      p->allocs.push_back(q);
-      df[i] = q;
-    }
-  }
-  if (hipEventCreate(&p->ev0) != hipSuccess || hipEventCreate(&p->ev1) != hipSuccess) return fail(CLOUDSC_EHIP);
-  *out = p;
-  return CLOUDSC_OK;
-}
-
-int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* ms) {
-  if (!p) return CLOUDSC_EINVAL;
-  int rc = validate_run_args(p->device, p->precision, variant, p->ngptot, p->nproma, p->klev);
-  if (rc) return rc;
-  HIPCHK(hipSetDevice(p->device));
-  const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
-  // workspaces for the chunk size (SCC / KSEG), allocated on first use
-  for (auto& s : p->slots) {
-    if (variant == CLOUDSC_VARIANT_KCACHE || s.scratch_variant == variant) continue;
-    const long long nb = cloudsc_gpu_scratch_bytes(p->precision, variant, p->chunk_blocks * p->nproma, p->nproma,
-                                                   p->klev);
-    if (nb <= 0) return CLOUDSC_EINVAL;
-    if ((size_t)nb > s.scratch_bytes) {
-      void* q = nullptr;
-      if (hipMalloc(&q, (size_t)nb) != hipSuccess) return CLOUDSC_ENOMEM;
-      p->allocs.push_back(q);
-      s.scratch = q;
-      s.scratch_bytes = (size_t)nb;
-    }
-    s.scratch_variant = variant;
-  }
-  const void* const* hf = (const void* const*)&p->host;
-  // all streams start after ev0 (recorded on the null stream) and ev1 waits for all of them
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipEventRecord(p->ev0, nullptr));
-  for (auto& s : p->slots) HIPCHK(hipStreamWaitEvent(s.st, p->ev0, 0));
-  for (int c = 0; c < nchunks && rc == CLOUDSC_OK; c++) {
-    auto& s = p->slots[c % p->nstreams];
-    const int b0 = c * p->chunk_blocks;
-    const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
-    const long long col0 = (long long)b0 * p->nproma;
-    const int ncols = (int)((col0 + (long long)nb * p->nproma <= p->ngptot) ? (long long)nb * p->nproma
-                                                                            : p->ngptot - col0);
-    void* const* df = (void* const*)&s.dev;
-    for (int i = 0; i < kNumFields; i++) {
-      const FieldDesc& d = kFieldTable[i];
-      if (!hf[i] || d.dir == FD_OUT) continue;
-      const size_t eb = d.is_int ? sizeof(int) : p->es;
-      const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * eb;
-      HIPCHK(hipMemcpyAsync(df[i], (const char*)hf[i] + (size_t)b0 * per, (size_t)nb * per, hipMemcpyHostToDevice,
-                            s.st));
-    }
-    rc = cloudsc_gpu_run(p->device, s.st, p->precision, variant, ncols, p->nproma, p->klev, &s.dev, s.scratch);
-    if (rc) break;
-    for (int i = 0; i < kNumFields; i++) {
-      const FieldDesc& d = kFieldTable[i];
-      if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
-      const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * p->es;
-      HIPCHK(hipMemcpyAsync((char*)hf[i] + (size_t)b0 * per, df[i], (size_t)nb * per, hipMemcpyDeviceToHost, s.st));
-    }
-  }
-  for (auto& s : p->slots) {
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(e, s.st));
-    HIPCHK(hipStreamWaitEvent(nullptr, e, 0));
-    (void)hipEventDestroy(e);
-  }
-  HIPCHK(hipEventRecord(p->ev1, nullptr));
-  HIPCHK(hipEventSynchronize(p->ev1));
-  if (rc) return rc;
-  float t = 0.f;
-  HIPCHK(hipEventElapsedTime(&t, p->ev0, p->ev1));
-  if (ms) *ms = t;
-  return CLOUDSC_OK;
-}
-
-int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p) {
-  if (!p) return CLOUDSC_EINVAL;
-  (void)hipSetDevice(p->device);
-  for (auto& s : p->slots)
-    if (s.st) { (void)hipStreamSynchronize(s.st); (void)hipStreamDestroy(s.st); }
-  for (void* q : p->allocs) (void)hipFree(q);
-  for (void* h : p->pinned) (void)hipHostUnregister(h);
-  if (p->ev0) (void)hipEventDestroy(p->ev0);
-  if (p->ev1) (void)hipEventDestroy(p->ev1);
-  delete p;
-  return CLOUDSC_OK;
-}
-
-}  // extern "C"

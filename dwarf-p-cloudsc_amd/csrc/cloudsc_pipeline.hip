@@ -1,0 +1,208 @@
+// cloudsc_pipeline.hip -- the host-buffer pipeline of include/cloudsc_amd.h
+// (cloudsc_host_pipeline_*).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "cloudsc_amd.h"
+#include "cloudsc_internal.h"
+
+using namespace cloudsc_impl;
+
+// ---------------------------------------------------------------------------
+// C ABI: host-buffer pipeline
+// ---------------------------------------------------------------------------
+// The reference GPU drivers copy every block-layout host array to the device,
+// run, and copy the outputs back (cloudsc_driver.cu:344-456; the "field"
+// variant of README.md:311-330 overlaps them).  Here the blocks are cut into
+// chunks of `chunk_blocks` NPROMA blocks -- one contiguous range of every
+// field, because the layout is block-major -- and chunk c runs on stream
+// c % nstreams: H2D of its inputs, the kernel, D2H of its outputs.  The host
+// arrays are pinned in place (hipHostRegister) once, at creation.
+namespace {
+
+enum FieldKind { FK_LEVEL, FK_HALF, FK_SPECIES, FK_SURFACE };
+enum FieldDir { FD_IN, FD_INOUT, FD_OUT, FD_AEROSOL };
+struct FieldDesc { int kind, dir, is_int; };
+// cloudsc_fields_t member order (include/cloudsc_amd.h)
+constexpr FieldDesc kFieldTable[] = {
+    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_IN, 0},   {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_HALF, FD_IN, 0},    {FK_SURFACE, FD_IN, 0}, {FK_SURFACE, FD_IN, 1}, {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
+    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
+    {FK_LEVEL, FD_INOUT, 0},
+    {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_SPECIES, FD_OUT, 0},
+    {FK_LEVEL, FD_OUT, 0},  {FK_SURFACE, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0}};
+constexpr int kNumFields = (int)(sizeof(kFieldTable) / sizeof(kFieldTable[0]));
+static_assert(sizeof(cloudsc_fields_t) == kNumFields * sizeof(void*), "field table out of sync with the header");
+
+size_t per_block_elems(int kind, int nproma, int klev) {
+  switch (kind) {
+    case FK_LEVEL: return (size_t)klev * nproma;
+    case FK_HALF: return (size_t)(klev + 1) * nproma;
+    case FK_SPECIES: return (size_t)CLOUDSC_NCLV * klev * nproma;
+    default: return (size_t)nproma;
+  }
+}
+
+}  // namespace
+
+struct cloudsc_host_pipeline {
+  int device, precision, ngptot, nproma, klev, nblocks, chunk_blocks, nstreams;
+  size_t es;
+  cloudsc_fields_t host;
+  std::vector<void*> pinned;
+  struct Slot {
+    hipStream_t st = nullptr;
+    cloudsc_fields_t dev{};
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    int scratch_variant = 0;
+  };
+  std::vector<Slot> slots;
+  std::vector<void*> allocs;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+extern "C" {
+
+int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p);
+
+int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int precision, int ngptot, int nproma,
+                                 int klev, int chunk_blocks, int nstreams, const cloudsc_fields_t* host) {
+  if (!out || !host || chunk_blocks <= 0 || nstreams <= 0 || nstreams > 16) return CLOUDSC_EINVAL;
+  *out = nullptr;
+  int rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KCACHE, ngptot, nproma, klev);
+  if (rc) return rc;
+  if (!fields_complete(host)) return CLOUDSC_EINVAL;
+  cloudsc_host_pipeline* p = new cloudsc_host_pipeline();
+  p->device = device; p->precision = precision; p->ngptot = ngptot; p->nproma = nproma; p->klev = klev;
+  p->nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  p->chunk_blocks = chunk_blocks < p->nblocks ? chunk_blocks : p->nblocks;
+  p->nstreams = nstreams;
+  p->es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
+  p->host = *host;
+  auto fail = [&](int r) { cloudsc_host_pipeline_destroy(p); return r; };
+  if (hipSetDevice(device) != hipSuccess) return fail(CLOUDSC_ENODEV);
+  void* const* hf = (void* const*)&p->host;
+  // pin the caller's arrays in place (already-pinned memory is fine)
+  for (int i = 0; i < kNumFields; i++) {
+    if (!hf[i]) continue;
+    const FieldDesc& d = kFieldTable[i];
+    const size_t bytes = (size_t)p->nblocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : p->es);
+    hipError_t e = hipHostRegister(hf[i], bytes, hipHostRegisterDefault);
+    if (e == hipSuccess) p->pinned.push_back(hf[i]);
+    else if (e != hipErrorHostMemoryAlreadyRegistered) { hip_fail(e, "hipHostRegister"); return fail(CLOUDSC_EHIP); }
+    else (void)hipGetLastError();
+  }
+  p->slots.resize(nstreams);
+  for (auto& s : p->slots) {
+    if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
+    void** df = (void**)&s.dev;
+    for (int i = 0; i < kNumFields; i++) {
+      if (!hf[i]) continue;
+      const FieldDesc& d = kFieldTable[i];
+      const size_t bytes =
+          (size_t)p->chunk_blocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : p->es);
+      void* q = nullptr;
+      if (hipMalloc(&q, bytes) != hipSuccess) { hip_fail(hipErrorOutOfMemory, "hipMalloc"); return fail(CLOUDSC_ENOMEM); }
+      p->allocs.push_back(q);
+      df[i] = q;
+    }
+  }
+  if (hipEventCreate(&p->ev0) != hipSuccess || hipEventCreate(&p->ev1) != hipSuccess) return fail(CLOUDSC_EHIP);
+  *out = p;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* ms) {
+  if (!p) return CLOUDSC_EINVAL;
+  int rc = validate_run_args(p->device, p->precision, variant, p->ngptot, p->nproma, p->klev);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(p->device));
+  const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
+  // workspaces for the chunk size (SCC / KSEG), allocated on first use
+  for (auto& s : p->slots) {
+    if (variant == CLOUDSC_VARIANT_KCACHE || s.scratch_variant == variant) continue;
+    const long long nb = cloudsc_gpu_scratch_bytes(p->precision, variant, p->chunk_blocks * p->nproma, p->nproma,
+                                                   p->klev);
+    if (nb <= 0) return CLOUDSC_EINVAL;
+    if ((size_t)nb > s.scratch_bytes) {
+      void* q = nullptr;
+      if (hipMalloc(&q, (size_t)nb) != hipSuccess) return CLOUDSC_ENOMEM;
+      p->allocs.push_back(q);
+      s.scratch = q;
+      s.scratch_bytes = (size_t)nb;
+    }
+    s.scratch_variant = variant;
+  }
+  const void* const* hf = (const void* const*)&p->host;
+  // all streams start after ev0 (recorded on the null stream) and ev1 waits for all of them
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipEventRecord(p->ev0, nullptr));
+  for (auto& s : p->slots) HIPCHK(hipStreamWaitEvent(s.st, p->ev0, 0));
+  for (int c = 0; c < nchunks && rc == CLOUDSC_OK; c++) {
+    auto& s = p->slots[c % p->nstreams];
+    const int b0 = c * p->chunk_blocks;
+    const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
+    const long long col0 = (long long)b0 * p->nproma;
+    const int ncols = (int)((col0 + (long long)nb * p->nproma <= p->ngptot) ? (long long)nb * p->nproma
+                                                                            : p->ngptot - col0);
+    void* const* df = (void* const*)&s.dev;
+    for (int i = 0; i < kNumFields; i++) {
+      const FieldDesc& d = kFieldTable[i];
+      if (!hf[i] || d.dir == FD_OUT) continue;
+      const size_t eb = d.is_int ? sizeof(int) : p->es;
+      const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * eb;
+      HIPCHK(hipMemcpyAsync(df[i], (const char*)hf[i] + (size_t)b0 * per, (size_t)nb * per, hipMemcpyHostToDevice,
+                            s.st));
+    }
+    rc = cloudsc_gpu_run(p->device, s.st, p->precision, variant, ncols, p->nproma, p->klev, &s.dev, s.scratch);
+    if (rc) break;
+    for (int i = 0; i < kNumFields; i++) {
+      const FieldDesc& d = kFieldTable[i];
+      if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
+      const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * p->es;
+      HIPCHK(hipMemcpyAsync((char*)hf[i] + (size_t)b0 * per, df[i], (size_t)nb * per, hipMemcpyDeviceToHost, s.st));
+    }
+  }
+  for (auto& s : p->slots) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e, s.st));
+    HIPCHK(hipStreamWaitEvent(nullptr, e, 0));
+    (void)hipEventDestroy(e);
+  }
+  HIPCHK(hipEventRecord(p->ev1, nullptr));
+  HIPCHK(hipEventSynchronize(p->ev1));
+  if (rc) return rc;
+  float t = 0.f;
+  HIPCHK(hipEventElapsedTime(&t, p->ev0, p->ev1));
+  if (ms) *ms = t;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p) {
+  if (!p) return CLOUDSC_EINVAL;
+  (void)hipSetDevice(p->device);
+  for (auto& s : p->slots)
+    if (s.st) { (void)hipStreamSynchronize(s.st); (void)hipStreamDestroy(s.st); }
+  for (void* q : p->allocs) (void)hipFree(q);
+  for (void* h : p->pinned) (void)hipHostUnregister(h);
+  if (p->ev0) (void)hipEventDestroy(p->ev0);
+  if (p->ev1) (void)hipEventDestroy(p->ev1);
+  delete p;
+  return CLOUDSC_OK;
+}
+
+}  // extern "C"
+

@@ -1,0 +1,363 @@
+// cloudsc_state.hip -- the device-resident dwarf state of include/cloudsc_amd.h
+// (cloudsc_state_*): on-device expansion of the KLON-column template (g % klon
+// of the GLOBAL column index), timed runs on the state's stream, and on-device
+// validation statistics against the KLON-column reference.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "cloudsc_amd.h"
+#include "cloudsc_internal.h"
+
+using namespace cloudsc_impl;
+
+// ---------------------------------------------------------------------------
+// plumbing kernels: expansion and validation statistics
+// ---------------------------------------------------------------------------
+// dst[b][L][i] = src[L][(col_offset + b*nproma + i) % klon], L < nlev
+template <typename T, typename S>
+__global__ void expand_kernel(T* __restrict__ dst, const S* __restrict__ src, int nlev, int klon,
+                              int nproma, long long col_offset, long long nblocks) {
+  const long long b = blockIdx.y;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nlev * nproma; e += gridDim.x * blockDim.x) {
+    const int L = e / nproma, i = e - L * nproma;
+    const long long g = col_offset + b * nproma + i;
+    dst[(size_t)b * nlev * nproma + e] = (T)src[(size_t)L * klon + (size_t)(g % klon)];
+  }
+  (void)nblocks;
+}
+
+// One workgroup per NPROMA block: min/max of the field, max|d|, sum|d|, sum|ref|
+// over the active lanes of that block (validate_mod.F90:136-146, with fabs).
+template <typename real>
+__global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld, const double* __restrict__ ref,
+                                                    int nlev, int klon, int nproma, long long ngptot,
+                                                    long long col_offset, double* __restrict__ part) {
+  const long long b = blockIdx.x;
+  const long long bsize = (ngptot - b * nproma) < nproma ? (ngptot - b * nproma) : nproma;
+  double mn = __DBL_MAX__, mx = -__DBL_MAX__, me = 0.0, es = 0.0, rs = 0.0;
+  for (int e = threadIdx.x; e < nlev * nproma; e += blockDim.x) {
+    const int L = e / nproma, i = e - L * nproma;
+    if (i >= bsize) continue;
+    const long long g = col_offset + b * nproma + i;
+    const double v = (double)fld[(size_t)b * nlev * nproma + e];
+    const double r = ref[(size_t)L * klon + (size_t)(g % klon)];
+    const double d = fabs(v - r);
+    mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, d); es += d; rs += fabs(r);
+  }
+  __shared__ double s[5][256];
+  s[0][threadIdx.x] = mn; s[1][threadIdx.x] = mx; s[2][threadIdx.x] = me; s[3][threadIdx.x] = es; s[4][threadIdx.x] = rs;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const int t = threadIdx.x;
+      s[0][t] = fmin(s[0][t], s[0][t + w]); s[1][t] = fmax(s[1][t], s[1][t + w]);
+      s[2][t] = fmax(s[2][t], s[2][t + w]); s[3][t] += s[3][t + w]; s[4][t] += s[4][t + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 5; q++) part[b * 5 + q] = s[q][0];
+}
+
+// ---------------------------------------------------------------------------
+// C ABI: device-resident dwarf state
+// ---------------------------------------------------------------------------
+struct cloudsc_gpu_state {
+  int device, precision, ngptot, nproma, klev, klon, nblocks;
+  long long col_offset;
+  size_t es;                      // element size
+  hipStream_t stream;
+  hipEvent_t ev0, ev1;
+  cloudsc_fields_t f;             // device pointers
+  void* plude_pristine;
+  void* scratch;                  // SCC temporaries
+  void* kseg_ws;                  // KSEG counter, flags and carried state
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+size_t field_elems(const cloudsc_gpu_state* s, int kind /*0 2d,1 2dh,2 3d,3 1d*/) {
+  const size_t nb = s->nblocks, np = s->nproma, kl = s->klev;
+  switch (kind) {
+    case 0: return nb * kl * np;
+    case 1: return nb * (kl + 1) * np;
+    case 2: return nb * 5 * kl * np;
+    default: return nb * np;
+  }
+}
+// validated field table: pointer slot and shape kind, in cloudsc_field_id order
+void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
+  const cloudsc_fields_t& f = s->f;
+  static const int kinds[CLOUDSC_NVALID] = {0, 0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 2};
+  void* const* slots[CLOUDSC_NVALID] = {
+      &f.plude, &f.pcovptot, &f.prainfrac_toprfz, &f.pfsqlf, &f.pfsqif, &f.pfcqlng, &f.pfcqnng,
+      &f.pfsqrf, &f.pfsqsf, &f.pfcqrng, &f.pfcqsng, &f.pfsqltur, &f.pfsqitur, &f.pfplsl, &f.pfplsn,
+      &f.pfhpsl, &f.pfhpsn, &f.tendency_loc_a, &f.tendency_loc_q, &f.tendency_loc_t, &f.tendency_loc_cld};
+  *kind = kinds[id];
+  return slots[id];
+}
+
+int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
+  s->allocs.push_back(*p);
+  return CLOUDSC_OK;
+}
+
+// upload one template array and expand it into the block-layout device field
+int expand_into(cloudsc_gpu_state* s, void* dst, const void* host_src, int nlev, bool is_int) {
+  const size_t src_bytes = (size_t)nlev * s->klon * (is_int ? sizeof(int) : sizeof(double));
+  void* d_src = nullptr;
+  HIPCHK(hipMalloc(&d_src, src_bytes));
+  hipError_t e = hipMemcpyAsync(d_src, host_src, src_bytes, hipMemcpyHostToDevice, s->stream);
+  if (e == hipSuccess) {
+    const int per = nlev * s->nproma;
+    dim3 grid((per + 255) / 256, s->nblocks);
+    if (is_int)
+      hipLaunchKernelGGL((expand_kernel<int, int>), grid, dim3(256), 0, s->stream, (int*)dst, (const int*)d_src,
+                         nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
+    else if (s->precision == CLOUDSC_FP64)
+      hipLaunchKernelGGL((expand_kernel<double, double>), grid, dim3(256), 0, s->stream, (double*)dst,
+                         (const double*)d_src, nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
+    else
+      hipLaunchKernelGGL((expand_kernel<float, double>), grid, dim3(256), 0, s->stream, (float*)dst,
+                         (const double*)d_src, nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  }
+  (void)hipFree(d_src);
+  if (e != hipSuccess) return hip_fail(e, "expand");
+  return CLOUDSC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, int ngptot, int nproma,
+                         long long col_offset, const cloudsc_template_t* t, const cloudsc_params_t* params) {
+  if (!out || !t || !params || col_offset < 0) return CLOUDSC_EINVAL;
+  *out = nullptr;
+  int rc = cloudsc_gpu_init(device, params);
+  if (rc) return rc;
+  rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KCACHE, ngptot, nproma, t->klev);
+  if (rc) return rc;
+  if (t->klon <= 0) return CLOUDSC_EINVAL;
+  const void* req[] = {t->pt, t->pq, t->tendency_tmp_t, t->tendency_tmp_q, t->tendency_tmp_a,
+                       t->tendency_tmp_cld, t->pvfl, t->pvfi, t->phrsw, t->phrlw, t->pvervel, t->pap,
+                       t->paph, t->plsm, t->ktype, t->plu, t->plude, t->psnde, t->pmfu, t->pmfd, t->pa,
+                       t->pclv, t->psupsat};
+  for (const void* q : req)
+    if (!q) return CLOUDSC_EINVAL;
+  if (params->laericesed && !t->pre_ice) return CLOUDSC_EINVAL;
+  if (params->laericeauto && (!t->picrit_aer || !t->pnice)) return CLOUDSC_EINVAL;
+
+  cloudsc_gpu_state* s = new cloudsc_gpu_state();
+  s->device = device; s->precision = precision; s->ngptot = ngptot; s->nproma = nproma;
+  s->klev = t->klev; s->klon = t->klon; s->col_offset = col_offset;
+  s->nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  s->es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
+  std::memset(&s->f, 0, sizeof(s->f));
+  auto fail = [&](int r) { cloudsc_state_destroy(s); return r; };
+  if (hipSetDevice(device) != hipSuccess) return fail(CLOUDSC_ENODEV);
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
+  if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) return fail(CLOUDSC_EHIP);
+
+  const size_t n2 = field_elems(s, 0) * s->es, n2h = field_elems(s, 1) * s->es;
+  const size_t n3 = field_elems(s, 2) * s->es, n1 = field_elems(s, 3) * s->es;
+  const int kl = s->klev;
+  struct In { const void** dst; const void* src; int nlev; size_t bytes; bool is_int; };
+  cloudsc_fields_t& f = s->f;
+  void* plude_dev = nullptr;
+  In ins[] = {
+      {&f.pt, t->pt, kl, n2, false}, {&f.pq, t->pq, kl, n2, false},
+      {&f.tendency_tmp_t, t->tendency_tmp_t, kl, n2, false}, {&f.tendency_tmp_q, t->tendency_tmp_q, kl, n2, false},
+      {&f.tendency_tmp_a, t->tendency_tmp_a, kl, n2, false}, {&f.tendency_tmp_cld, t->tendency_tmp_cld, 5 * kl, n3, false},
+      {&f.pvfl, t->pvfl, kl, n2, false}, {&f.pvfi, t->pvfi, kl, n2, false}, {&f.phrsw, t->phrsw, kl, n2, false},
+      {&f.phrlw, t->phrlw, kl, n2, false}, {&f.pvervel, t->pvervel, kl, n2, false}, {&f.pap, t->pap, kl, n2, false},
+      {&f.paph, t->paph, kl + 1, n2h, false}, {&f.plsm, t->plsm, 1, n1, false},
+      {(const void**)&f.ktype, t->ktype, 1, (size_t)s->nblocks * nproma * sizeof(int), true},
+      {&f.plu, t->plu, kl, n2, false}, {&f.psnde, t->psnde, kl, n2, false}, {&f.pmfu, t->pmfu, kl, n2, false},
+      {&f.pmfd, t->pmfd, kl, n2, false}, {&f.pa, t->pa, kl, n2, false}, {&f.pclv, t->pclv, 5 * kl, n3, false},
+      {&f.psupsat, t->psupsat, kl, n2, false},
+      {&f.plcrit_aer, t->plcrit_aer, kl, n2, false}, {&f.picrit_aer, t->picrit_aer, kl, n2, false},
+      {&f.pre_ice, t->pre_ice, kl, n2, false}, {&f.pccn, t->pccn, kl, n2, false}, {&f.pnice, t->pnice, kl, n2, false},
+      {(const void**)&plude_dev, t->plude, kl, n2, false},
+  };
+  for (In& in : ins) {
+    if (!in.src) continue;
+    void* p = nullptr;
+    if ((rc = dalloc(s, &p, in.bytes))) return fail(rc);
+    if ((rc = expand_into(s, p, in.src, in.nlev, in.is_int))) return fail(rc);
+    *in.dst = p;
+  }
+  s->plude_pristine = plude_dev;
+  struct Out { void** dst; size_t bytes; };
+  Out outs[] = {{&f.plude, n2}, {&f.tendency_loc_t, n2}, {&f.tendency_loc_q, n2}, {&f.tendency_loc_a, n2},
+                {&f.tendency_loc_cld, n3}, {&f.pcovptot, n2}, {&f.prainfrac_toprfz, n1},
+                {&f.pfsqlf, n2h}, {&f.pfsqif, n2h}, {&f.pfcqnng, n2h}, {&f.pfcqlng, n2h}, {&f.pfsqrf, n2h},
+                {&f.pfsqsf, n2h}, {&f.pfcqrng, n2h}, {&f.pfcqsng, n2h}, {&f.pfsqltur, n2h}, {&f.pfsqitur, n2h},
+                {&f.pfplsl, n2h}, {&f.pfplsn, n2h}, {&f.pfhpsl, n2h}, {&f.pfhpsn, n2h}};
+  for (Out& o : outs) {
+    if ((rc = dalloc(s, o.dst, o.bytes))) return fail(rc);
+    if (hipMemsetAsync(*o.dst, 0xff, o.bytes, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);  // NaN
+  }
+  if (hipMemcpyAsync(f.plude, s->plude_pristine, n2, hipMemcpyDeviceToDevice, s->stream) != hipSuccess)
+    return fail(CLOUDSC_EHIP);
+  if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);
+  *out = s;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_fields(const cloudsc_gpu_state_t* s, cloudsc_fields_t* out) {
+  if (!s || !out) return CLOUDSC_EINVAL;
+  *out = s->f;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_reset(cloudsc_gpu_state_t* s) {
+  if (!s) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipMemcpyAsync(s->f.plude, s->plude_pristine, field_elems(s, 0) * s->es, hipMemcpyDeviceToDevice,
+                        s->stream));
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) {
+  if (!s || reps <= 0) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  void* scratch = nullptr;
+  if (variant == CLOUDSC_VARIANT_SCC || variant == CLOUDSC_VARIANT_KSEG) {   // workspaces, allocated on first use
+    void*& ws = variant == CLOUDSC_VARIANT_SCC ? s->scratch : s->kseg_ws;
+    if (!ws) {
+      const long long nb = cloudsc_gpu_scratch_bytes(s->precision, variant, s->ngptot, s->nproma, s->klev);
+      if (nb <= 0) return CLOUDSC_EINVAL;
+      int rc0 = dalloc(s, &ws, (size_t)nb);
+      if (rc0) return rc0;
+    }
+    scratch = ws;
+  }
+  std::vector<hipEvent_t> ev(2 * (size_t)reps);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  int rc = CLOUDSC_OK;
+  for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
+    // out of place: every step reads the pristine plude and writes the INOUT
+    // result to f.plude, so repeated steps see the same input with no restore copy
+    HIPCHK(hipEventRecord(ev[2 * r], s->stream));
+    rc = gpu_run_impl(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f, scratch,
+                      s->plude_pristine);
+    HIPCHK(hipEventRecord(ev[2 * r + 1], s->stream));
+  }
+  hipError_t e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess && rc == CLOUDSC_OK) rc = hip_fail(e, "hipStreamSynchronize");
+  for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
+    float t = 0.f;
+    e = hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]);
+    if (e != hipSuccess) rc = hip_fail(e, "hipEventElapsedTime");
+    if (ms) ms[r] = t;
+  }
+  for (auto& x : ev) (void)hipEventDestroy(x);
+  if (rc == CLOUDSC_OK && variant == CLOUDSC_VARIANT_KSEG) {
+    // a segment whose predecessor never arrived gives up after a bounded spin
+    // and counts itself here: its results are invalid
+    unsigned err = 0;
+    HIPCHK(hipMemcpy(&err, (unsigned*)scratch + 1, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+      char msg[96];
+      std::snprintf(msg, sizeof(msg), "KSEG: %u segment hand-offs timed out", err);
+      set_error_text(msg);
+      rc = CLOUDSC_EHIP;
+    }
+  }
+  return rc;
+}
+
+int cloudsc_state_sync(cloudsc_gpu_state_t* s) {
+  if (!s) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return CLOUDSC_OK;
+}
+
+long long cloudsc_state_field_elems(const cloudsc_gpu_state_t* s, int id) {
+  if (!s || id < 0 || id >= CLOUDSC_NVALID) return -1;
+  int kind;
+  valid_slot(s, id, &kind);
+  return (long long)field_elems(s, kind);
+}
+
+int cloudsc_state_download(cloudsc_gpu_state_t* s, int id, double* host) {
+  if (!s || !host || id < 0 || id >= CLOUDSC_NVALID) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  int kind;
+  void* const* slot = valid_slot(s, id, &kind);
+  const size_t n = field_elems(s, kind);
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (s->precision == CLOUDSC_FP64) {
+    HIPCHK(hipMemcpy(host, *slot, n * sizeof(double), hipMemcpyDeviceToHost));
+  } else {
+    std::vector<float> tmp(n);
+    HIPCHK(hipMemcpy(tmp.data(), *slot, n * sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; i++) host[i] = tmp[i];
+  }
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* ref, cloudsc_stats_t* stats) {
+  if (!s || !ref || !stats || ref->klon <= 0 || ref->klev != s->klev) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  double* part = nullptr;
+  double* dref = nullptr;
+  HIPCHK(hipMalloc(&part, (size_t)s->nblocks * 5 * sizeof(double)));
+  const size_t max_ref = (size_t)5 * (s->klev + 1) * ref->klon;
+  hipError_t e = hipMalloc(&dref, max_ref * sizeof(double));
+  std::vector<double> h((size_t)s->nblocks * 5);
+  for (int id = 0; id < CLOUDSC_NVALID && e == hipSuccess; id++) {
+    int kind;
+    void* const* slot = valid_slot(s, id, &kind);
+    const int nlev = kind == 0 ? s->klev : kind == 1 ? s->klev + 1 : kind == 2 ? 5 * s->klev : 1;
+    if (!ref->field[id]) { e = hipErrorInvalidValue; break; }
+    e = hipMemcpy(dref, ref->field[id], (size_t)nlev * ref->klon * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) break;
+    if (s->precision == CLOUDSC_FP64)
+      hipLaunchKernelGGL(stats_kernel<double>, dim3(s->nblocks), dim3(256), 0, s->stream, (const double*)*slot,
+                         dref, nlev, ref->klon, s->nproma, (long long)s->ngptot, s->col_offset, part);
+    else
+      hipLaunchKernelGGL(stats_kernel<float>, dim3(s->nblocks), dim3(256), 0, s->stream, (const float*)*slot,
+                         dref, nlev, ref->klon, s->nproma, (long long)s->ngptot, s->col_offset, part);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) break;
+    cloudsc_stats_t t = {__DBL_MAX__, -__DBL_MAX__, 0.0, 0.0, 0.0};
+    for (int b = 0; b < s->nblocks; b++) {            // block order: deterministic
+      t.minval = fmin(t.minval, h[b * 5 + 0]); t.maxval = fmax(t.maxval, h[b * 5 + 1]);
+      t.maxerr = fmax(t.maxerr, h[b * 5 + 2]); t.errsum += h[b * 5 + 3]; t.refsum += h[b * 5 + 4];
+    }
+    stats[id] = t;
+  }
+  (void)hipFree(part);
+  (void)hipFree(dref);
+  if (e != hipSuccess) return hip_fail(e, "validate");
+  return CLOUDSC_OK;
+}
+
+int cloudsc_state_destroy(cloudsc_gpu_state_t* s) {
+  if (!s) return CLOUDSC_OK;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (void* p : s->allocs) (void)hipFree(p);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+  return CLOUDSC_OK;
+}
+
+}  // extern "C"
+

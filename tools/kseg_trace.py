@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: schedule of the persistent segmented kernel (KSEG) from the trace
-build (build/libkseg_trace.so, -DCLOUDSC_KSEG_TRACE): per-item start/end on the
+build (build/libkseg_trace.so: make -C dwarf-p-cloudsc_amd variant
+VFLAGS=-DCLOUDSC_KSEG_TRACE OUT=../build/libkseg_trace.so): per-item start/end on the
 100 MHz realtime clock, workgroup and XCC.  Prints per-segment item durations,
 the makespan, the workgroups' busy fraction and the tail."""
 import ctypes as C
