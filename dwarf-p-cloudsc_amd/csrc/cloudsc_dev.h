@@ -12,6 +12,8 @@
 
 #include <type_traits>
 
+#include "cloudsc_libm.h"
+
 namespace cloudsc {
 
 template <typename real>
@@ -86,6 +88,73 @@ __device__ __forceinline__ T launder_vgpr(T v) {
 // Device math used by the kernels.  One place to swap implementations; the
 // CLOUDSC_ABLATE_* macros exist only for timing-only diagnostic builds (they
 // give wrong results) that price each function's share of the kernel.
+//
+// fp64 exp/pow: the reference CPU build's own algorithms (cloudsc_libm.h),
+// so that the GPU rounds every exp/pow exactly as the reference kernel does.
+// Their tables (5 KB) are copied from __constant__ memory into LDS at the start
+// of every physics kernel (libm_tables_to_lds) and read there with per-lane
+// indices: one ds_read_b128 per exp, b128 + b64 per log of a pow.  A table
+// read from global memory instead would be counted by vmcnt, and waiting for
+// it inside a physics branch would drain the software-pipelined level loads
+// (vmcnt(0)); LDS reads are counted by lgkmcnt.
+// CLOUDSC_OCML_EXP_POW selects OCML's exp/powr instead (about 1 ulp, not the
+// reference's rounding).
+__constant__ __attribute__((aligned(16))) unsigned long long g_cl_exp_tab[2 * 128] = {CLOUDSC_LIBM_EXP_TAB};
+__constant__ __attribute__((aligned(16))) double g_cl_log_tab[4 * 128] = {CLOUDSC_LIBM_LOG_TAB};
+typedef unsigned long long cl_u64x2 __attribute__((ext_vector_type(2)));
+typedef double cl_f64x2 __attribute__((ext_vector_type(2)));
+__shared__ cl_u64x2 s_cl_exp_tab[128];       // {tail, sbits}
+__shared__ cl_f64x2 s_cl_log_tab[128];       // {invc, logc}
+__shared__ double s_cl_logtail_tab[128];     // logctail
+struct LdsLibmTabs {
+  __device__ __forceinline__ cloudsc_libm::ExpEntry exp_entry(uint32_t k) const {
+    const cl_u64x2 e = s_cl_exp_tab[k];
+    return {e.x, e.y};
+  }
+  __device__ __forceinline__ cloudsc_libm::LogEntry log_entry(uint32_t i) const {
+    const cl_f64x2 a = s_cl_log_tab[i];
+    return {a.x, a.y, s_cl_logtail_tab[i]};
+  }
+};
+// The complete functions, out of line, for the arguments outside the hot
+// range (tables from __constant__ memory; never taken by CLOUDSC's data).
+struct ConstLibmTabs {
+  __device__ __forceinline__ cloudsc_libm::ExpEntry exp_entry(uint32_t k) const {
+    const cl_u64x2 e = ((const cl_u64x2*)g_cl_exp_tab)[k];
+    return {e.x, e.y};
+  }
+  __device__ __forceinline__ cloudsc_libm::LogEntry log_entry(uint32_t i) const {
+    const cl_f64x2 a = ((const cl_f64x2*)g_cl_log_tab)[2 * i];
+    return {a.x, a.y, g_cl_log_tab[4 * i + 2]};
+  }
+};
+#ifdef CLOUDSC_LIBM_COLD_INLINE   // experiment: cold paths inlined at every call site
+#define CLOUDSC_LIBM_COLD_ATTR __forceinline__
+#else
+#define CLOUDSC_LIBM_COLD_ATTR __noinline__ __attribute__((pure))
+#endif
+__device__ CLOUDSC_LIBM_COLD_ATTR double cl_exp_cold(double x) { return cloudsc_libm::exp(x, ConstLibmTabs{}); }
+__device__ CLOUDSC_LIBM_COLD_ATTR double cl_pow_cold(double x, double y) { return cloudsc_libm::pow(x, y, ConstLibmTabs{}); }
+struct DevLibmCold {
+  __device__ __forceinline__ double exp(double x) const { return cl_exp_cold(x); }
+  __device__ __forceinline__ double pow(double x, double y) const { return cl_pow_cold(x, y); }
+};
+// Every thread of the workgroup must call this before the physics (it ends in
+// a barrier).  fp32 kernels use OCML and need no tables.
+template <typename real>
+__device__ __forceinline__ void libm_tables_to_lds() {
+#ifndef CLOUDSC_OCML_EXP_POW
+  if constexpr (std::is_same<real, double>::value) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+      s_cl_exp_tab[i] = ((const cl_u64x2*)g_cl_exp_tab)[i];
+      s_cl_log_tab[i] = ((const cl_f64x2*)g_cl_log_tab)[2 * i];
+      s_cl_logtail_tab[i] = g_cl_log_tab[4 * i + 2];
+    }
+    __syncthreads();
+  }
+#endif
+}
+
 #ifdef CLOUDSC_NOINLINE_POW
 __device__ __attribute__((noinline)) double cl_pow_ool(double x, double y);
 __device__ __attribute__((noinline)) float cl_pow_ool(float x, float y);
@@ -96,8 +165,26 @@ __device__ __attribute__((noinline)) float cl_pow_ool(float x, float y);
 // core computation as pow without the special-case fix-ups.
 extern "C" __device__ double __ocml_powr_f64(double, double);
 extern "C" __device__ float __ocml_powr_f32(float, float);
-__device__ __forceinline__ double cl_powr(double x, double y) { return __ocml_powr_f64(x, y); }
+#ifdef CLOUDSC_OCML_EXP_POW
+#define CLOUDSC_OCML_EXP
+#define CLOUDSC_OCML_POW
+#endif
+__device__ __forceinline__ double cl_powr(double x, double y) {
+#ifdef CLOUDSC_OCML_POW
+  return __ocml_powr_f64(x, y);
+#else
+  return cloudsc_libm::pow_split(x, y, LdsLibmTabs{}, DevLibmCold{});
+#endif
+}
 __device__ __forceinline__ float cl_powr(float x, float y) { return __ocml_powr_f32(x, y); }
+__device__ __forceinline__ double cl_exp_impl(double x) {
+#ifdef CLOUDSC_OCML_EXP
+  return exp(x);
+#else
+  return cloudsc_libm::exp_split(x, LdsLibmTabs{}, DevLibmCold{});
+#endif
+}
+__device__ __forceinline__ float cl_exp_impl(float x) { return expf(x); }
 template <typename real>
 __device__ __forceinline__ real cl_pow(real x, real y) {
 #if defined(CLOUDSC_ABLATE_POW)
@@ -115,7 +202,7 @@ __device__ __forceinline__ real cl_exp(real x) {
 #ifdef CLOUDSC_ABLATE_EXP
   return x + (real)1.0;
 #else
-  return exp(x);
+  return cl_exp_impl(x);
 #endif
 }
 

@@ -161,18 +161,21 @@ bool fields_complete(const cloudsc_fields_t* f) {
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 __global__ void __launch_bounds__(256, WAVES) kcache_entry(const KArgs<real> a) {
   (void)a;
+  libm_tables_to_lds<real>();
   cloudsc_kcache_body<real, PF, AER, LDSC>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
                                            dev_params<real>());
 }
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 __global__ void __launch_bounds__(256, WAVES) kseg_entry(const KArgs<real> a, const PersistArgs<real> pa) {
   (void)a;
+  libm_tables_to_lds<real>();
   cloudsc_kcache_persistent_body<real, PF, AER, LDSC>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
                                                       dev_params<real>(), pa);
 }
 template <typename real, bool AER>
 __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccScratch<real> s) {
   (void)a;
+  libm_tables_to_lds<real>();
   cloudsc_scc_body<real, AER>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), s, dev_params<real>());
 }
 

@@ -411,3 +411,83 @@ def test_invalid_arguments(lib, ds):
         s.params[key] = val
         with pytest.raises(ca.CloudscError):
             ca.GpuState(s, 64, 64)
+
+
+# ---- bit-for-bit parity with the reference kernel (fp64) ----
+# The device exp/pow are the reference CPU build's own algorithms
+# (csrc/cloudsc_libm.h, checked against the host C library by tests/test_libm.py),
+# division is correctly rounded and no multiply-add is contracted, so the fp64
+# GPU kernels reproduce the reference kernel (and its restatement, the oracle)
+# bit for bit.  Scenario goldens W/M are the reference kernel's own outputs.
+def bitwise_mismatches(out, ref):
+    bad = {}
+    for _, k in ca.VALIDATED:
+        a = np.ascontiguousarray(out[k], dtype=np.float64).view(np.uint64)
+        r = np.ascontiguousarray(ref[k], dtype=np.float64).view(np.uint64)
+        n = int(np.count_nonzero(a != r))
+        if n:
+            bad[k] = (n, rel_l1(out[k], ref[k]))
+    return bad
+
+
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
+@pytest.mark.parametrize("ngptot,nproma", [(100, 128), (1000, 128), (1000, 64)])
+def test_bitwise_vs_oracle(lib, ds, oracle_mod, variant, ngptot, nproma):
+    out = run_gpu(ds, ngptot, nproma, variant=variant)
+    ref = oracle_outputs(oracle_mod, ds, ngptot, nproma)
+    assert bitwise_mismatches(out, ref) == {}
+
+
+@pytest.mark.parametrize("name", ["W", "M"])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG])
+def test_bitwise_vs_reference_kernel_scenarios(lib, scenarios, name, variant):
+    s = scenarios[name]
+    out = run_gpu(s, 100, 128, variant=variant)
+    assert bitwise_mismatches(out, s.reference) == {}
+
+
+def test_bitwise_vs_reference_kernel_built_here(lib, ds, oracle_mod):
+    # the unmodified reference kernel, compiled from its own sources (oracle/_ref)
+    if not oracle_mod.ref_available():
+        pytest.skip("oracle/_ref not built (no reference checkout at build time)")
+    st, _ = oracle_mod.run_ref(ds, 1000, 128)
+    ref = ca.state_outputs_to_template(st.arrays, 1000)
+    out = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KSEG)
+    assert bitwise_mismatches(out, ref) == {}
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_bitwise_random_perturbations(lib, ds, oracle_mod, seed):
+    import make_fixtures as mf
+    s = mf.perturbed(ds, seed)
+    out = run_gpu(s, 1000, 128, variant=ca.VARIANT_KSEG)
+    ref = oracle_outputs(oracle_mod, s, 1000, 128)
+    assert bitwise_mismatches(out, ref) == {}
+
+
+@pytest.mark.parametrize("case", ["nssopt0", "nssopt2", "nssopt3", "aerosol", "klev60"])
+def test_bitwise_other_configurations(lib, ds, oracle_mod, case):
+    import make_fixtures as mf
+    if case.startswith("nssopt"):
+        s = ds.copy()
+        s.params["nssopt"] = int(case[-1])
+    elif case == "aerosol":
+        s = mf.with_aerosols(ds)
+    else:
+        s = sliced_levels(ds, 77)
+    out = run_gpu(s, 300, 64, variant=ca.VARIANT_KSEG)
+    ref = oracle_outputs(oracle_mod, s, 300, 64)
+    assert bitwise_mismatches(out, ref) == {}
+
+
+def test_dwarf_tolerance_vs_reference_h5(lib, ds):
+    """The dwarf's own printed check (validate_mod.F90:273-290): relL1 of every
+    field vs reference.h5 within 10*eps(fp64), no '!!!!' flag."""
+    out = run_gpu(ds, 100, 128, variant=ca.VARIANT_KSEG)
+    eps = np.finfo(np.float64).eps
+    for name, k in ca.VALIDATED:
+        r = ds.reference[k].astype(np.float64)
+        d = np.abs(out[k] - r).sum()
+        s = np.abs(r).sum()
+        rel = 0.0 if d < eps else (d / s if s >= eps else d / (1.0 + s))
+        assert rel <= 10 * eps, (name, rel)
