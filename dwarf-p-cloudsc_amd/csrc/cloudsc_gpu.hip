@@ -188,7 +188,10 @@ template <typename real> int kcache_default_cfg();
 template <> int kcache_default_cfg<double>() { return 20; }    // 2 waves/SIMD, carried state in registers
 template <> int kcache_default_cfg<float>() { return 140; }   // 4 waves/SIMD, carried state in LDS
 template <typename real> int kseg_default_cfg();
-template <> int kseg_default_cfg<double>() { return 20; }
+// fp64 KSEG: 2 waves/SIMD, carried state in LDS, neighbour levels re-read (cfg
+// 122): with the LDS-table exp/pow it is 5-7 % faster than the register-carry
+// cfg 20 (profiles/r01/sweep_kseg_ldsc_libm.jsonl)
+template <> int kseg_default_cfg<double>() { return 122; }
 template <> int kseg_default_cfg<float>() { return 31; }      // 3 waves/SIMD, register prefetch
 
 
