@@ -22,8 +22,9 @@
 // physics needs one level ahead (paph, pmfu, pmfd, plu) two levels ahead.
 //
 // Arithmetic keeps the reference's operand order (hipcc -ffp-contract=off, so
-// no FMA contraction); the only expected differences vs the CPU are the
-// last-ulp results of OCML exp/pow vs glibc.
+// no FMA contraction), divisions are correctly rounded (cl_div) and fp64
+// exp/pow are the reference CPU build's own algorithms (cloudsc_libm.h): the
+// fp64 output is the reference kernel's, bit for bit.
 #pragma once
 #include "cloudsc_dev.h"
 #ifdef CLOUDSC_BRANCH_STATS

@@ -2,12 +2,13 @@
 the oracle (C restatement, itself bit-exact vs the reference C kernel) and the
 reference goldens (data/reference_*.dat == config-files/reference.h5).
 
-Tolerances (fp64).  The kernels keep the reference's operation order with no
-FMA contraction (-ffp-contract=off), so the only differences from the CPU are
-the last-ulp results of the device libm (OCML exp/pow) vs glibc.  SURVEY.md §8c
-measured what ulp-level perturbations of exp/pow do to this kernel: relL1 up to
-~2e-14.  The gate is relL1 <= 1e-12 per field and max|d| <= 1e-10 * max|ref|
-(the max-norm is looser because single points near thresholds amplify an ulp).
+fp64 is compared BIT FOR BIT (the bitwise_* tests at the end): the kernels
+keep the reference's operation order with no FMA contraction
+(-ffp-contract=off), divide with correct rounding, and evaluate exp/pow with
+the reference CPU build's own algorithms (csrc/cloudsc_libm.h).  The tolerance
+gates (relL1 <= 1e-12 per field, max|d| <= 1e-10 * max|ref|) remain for the
+wider shape/variant matrix; SURVEY.md §8c measured that ulp-level exp/pow
+perturbations move this kernel by relL1 ~2e-14.
 fp32: vs the fp32 CPU restatement relL1 <= 1e-3 per field (the algorithm has
 thresholds at 1e-14 / 1e-8 that float rounding crosses).
 """
