@@ -106,6 +106,26 @@ typedef double cl_f64x2 __attribute__((ext_vector_type(2)));
 __shared__ cl_u64x2 s_cl_exp_tab[128];       // {tail, sbits}
 __shared__ cl_f64x2 s_cl_log_tab[128];       // {invc, logc}
 __shared__ double s_cl_logtail_tab[128];     // logctail
+// single precision (expf/powf): 32 x 2^(i/32) bits, 16 x {invc, logc}
+__constant__ __attribute__((aligned(16))) unsigned long long g_cl_exp2f_tab[32] = {CLOUDSC_LIBM_EXP2F_TAB};
+__constant__ __attribute__((aligned(16))) double g_cl_powf_tab[2 * 16] = {CLOUDSC_LIBM_POWF_LOG2_TAB};
+__shared__ unsigned long long s_cl_exp2f_tab[32];
+__shared__ cl_f64x2 s_cl_powf_tab[16];
+struct LdsLibmTabsF {
+  __device__ __forceinline__ uint64_t exp2f_entry(uint32_t i) const { return s_cl_exp2f_tab[i]; }
+  __device__ __forceinline__ void powf_log2_entry(uint32_t i, double* invc, double* logc) const {
+    const cl_f64x2 a = s_cl_powf_tab[i];
+    *invc = a.x;
+    *logc = a.y;
+  }
+};
+struct ConstLibmTabsF {
+  __device__ __forceinline__ uint64_t exp2f_entry(uint32_t i) const { return g_cl_exp2f_tab[i]; }
+  __device__ __forceinline__ void powf_log2_entry(uint32_t i, double* invc, double* logc) const {
+    *invc = g_cl_powf_tab[2 * i];
+    *logc = g_cl_powf_tab[2 * i + 1];
+  }
+};
 struct LdsLibmTabs {
   __device__ __forceinline__ cloudsc_libm::ExpEntry exp_entry(uint32_t k) const {
     const cl_u64x2 e = s_cl_exp_tab[k];
@@ -135,12 +155,18 @@ struct ConstLibmTabs {
 #endif
 __device__ CLOUDSC_LIBM_COLD_ATTR double cl_exp_cold(double x) { return cloudsc_libm::exp(x, ConstLibmTabs{}); }
 __device__ CLOUDSC_LIBM_COLD_ATTR double cl_pow_cold(double x, double y) { return cloudsc_libm::pow(x, y, ConstLibmTabs{}); }
+__device__ CLOUDSC_LIBM_COLD_ATTR float cl_expf_cold(float x) { return cloudsc_libm::expf(x, ConstLibmTabsF{}); }
+__device__ CLOUDSC_LIBM_COLD_ATTR float cl_powf_cold(float x, float y) {
+  return cloudsc_libm::powf(x, y, ConstLibmTabsF{});
+}
 struct DevLibmCold {
   __device__ __forceinline__ double exp(double x) const { return cl_exp_cold(x); }
   __device__ __forceinline__ double pow(double x, double y) const { return cl_pow_cold(x, y); }
+  __device__ __forceinline__ float expf(float x) const { return cl_expf_cold(x); }
+  __device__ __forceinline__ float powf(float x, float y) const { return cl_powf_cold(x, y); }
 };
 // Every thread of the workgroup must call this before the physics (it ends in
-// a barrier).  fp32 kernels use OCML and need no tables.
+// a barrier).
 template <typename real>
 __device__ __forceinline__ void libm_tables_to_lds() {
 #ifndef CLOUDSC_OCML_EXP_POW
@@ -149,6 +175,12 @@ __device__ __forceinline__ void libm_tables_to_lds() {
       s_cl_exp_tab[i] = ((const cl_u64x2*)g_cl_exp_tab)[i];
       s_cl_log_tab[i] = ((const cl_f64x2*)g_cl_log_tab)[2 * i];
       s_cl_logtail_tab[i] = g_cl_log_tab[4 * i + 2];
+    }
+    __syncthreads();
+  } else {
+    for (int i = threadIdx.x; i < 32; i += blockDim.x) {
+      s_cl_exp2f_tab[i] = g_cl_exp2f_tab[i];
+      if (i < 16) s_cl_powf_tab[i] = ((const cl_f64x2*)g_cl_powf_tab)[i];
     }
     __syncthreads();
   }
@@ -176,7 +208,13 @@ __device__ __forceinline__ double cl_powr(double x, double y) {
   return cloudsc_libm::pow_split(x, y, LdsLibmTabs{}, DevLibmCold{});
 #endif
 }
-__device__ __forceinline__ float cl_powr(float x, float y) { return __ocml_powr_f32(x, y); }
+__device__ __forceinline__ float cl_powr(float x, float y) {
+#ifdef CLOUDSC_OCML_POW
+  return __ocml_powr_f32(x, y);
+#else
+  return cloudsc_libm::powf_split(x, y, LdsLibmTabsF{}, DevLibmCold{});
+#endif
+}
 __device__ __forceinline__ double cl_exp_impl(double x) {
 #ifdef CLOUDSC_OCML_EXP
   return exp(x);
@@ -184,7 +222,13 @@ __device__ __forceinline__ double cl_exp_impl(double x) {
   return cloudsc_libm::exp_split(x, LdsLibmTabs{}, DevLibmCold{});
 #endif
 }
-__device__ __forceinline__ float cl_exp_impl(float x) { return expf(x); }
+__device__ __forceinline__ float cl_exp_impl(float x) {
+#ifdef CLOUDSC_OCML_EXP
+  return expf(x);
+#else
+  return cloudsc_libm::expf_split(x, LdsLibmTabsF{}, DevLibmCold{});
+#endif
+}
 template <typename real>
 __device__ __forceinline__ real cl_pow(real x, real y) {
 #if defined(CLOUDSC_ABLATE_POW)

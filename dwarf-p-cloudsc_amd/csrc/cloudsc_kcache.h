@@ -204,7 +204,11 @@ __device__ __forceinline__ void init_level(const P& c, const LevelIn<real>& in, 
     s.zqx0[m] = zqx[m];
     zlneg[m] = R(0.0);
   }
-  real ttend = R(0.0), qtend = R(0.0);
+  // The zero is opaque to the optimiser: with it visible, the fp32 SCC build
+  // (packed v_pk_mul_f32 operands) folded (0 - a) - b into (-a) - b, which is
+  // -0 instead of +0 when a = b = 0 -- a sign-of-zero change the IEEE
+  // semantics (no nsz flag) do not allow.
+  real ttend = launder_vgpr(R(0.0)), qtend = launder_vgpr(R(0.0));
   // tidy up very small cloud cover or total cloud water (:519-541)
   if (zqx[QL] + zqx[QI] < c.rlmin || za < c.ramin) {
     real zqadj;
@@ -439,8 +443,14 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       real tt = fmax(ztp1 + zdtforc, R(160.0));
       real qsm = zqsmix;
       const real zqp = cl_div(R(1.0), pap_k);
+#ifdef CLOUDSC_ABLATE_NEWTON   // timing-only diagnostic build: the two Newton steps replaced by a cheap stand-in
+      tt = launder_vgpr(tt); qsm = qsm - R(1e-9) * tt * zqp;
+  #pragma unroll
+      for (int it = 0; it < 0; it++) {
+#else
   #pragma unroll
       for (int it = 0; it < 2; it++) {
+#endif
         const real a = foealfa<real>(c, tt);
         real zqsat = (c.r2es * (a * exp_liq<real>(c, tt) + (R(1.0) - a) * exp_ice<real>(c, tt))) * zqp;
         zqsat = fmin(R(0.5), zqsat);
@@ -720,6 +730,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // zsolqa[n][m] and its transpose zsolqa[m][n] (the diagonal twice).
     // The structurally-zero entries are kept as literal zeros so the
     // summation order (and hence rounding) matches the dense reference.
+#ifndef CLOUDSC_ABLATE_SINKS   // timing-only diagnostic build: no sink truncation (5.2)
     {
       real z = R(0.0), psum, zrat;
       // m = ql: zsolqa[n][ql] = {ll, il, rl, sl, vl}
@@ -760,6 +771,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       if (sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
       if (sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
     }
+#endif
 
     // 5.2.2 implicit solver (:2294-2397).  With the zsolqb sparsity above,
     //   zqlhs = I + diag(fallsink) + diag(row sums of zsolqb) - offdiag(zsolqb)

@@ -492,3 +492,33 @@ def test_dwarf_tolerance_vs_reference_h5(lib, ds):
         s = np.abs(r).sum()
         rel = 0.0 if d < eps else (d / s if s >= eps else d / (1.0 + s))
         assert rel <= 10 * eps, (name, rel)
+
+
+# fp32: the device expf/powf are the host C library's single-precision
+# algorithms too (csrc/cloudsc_libm.h), so the fp32 kernels reproduce the fp32
+# restatement (JPRB=sp semantics: float storage and constants, expf/powf) bit
+# for bit.
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
+def test_bitwise_fp32_vs_oracle(lib, ds, oracle_mod, variant):
+    out = run_gpu(ds, 1000, 128, precision=ca.FP32, variant=variant)
+    ref = oracle_outputs(oracle_mod, ds, 1000, 128, precision=ca.FP32)
+    bad = {}
+    for _, k in ca.VALIDATED:
+        a = np.ascontiguousarray(out[k], dtype=np.float32).view(np.uint32)
+        r = np.ascontiguousarray(ref[k], dtype=np.float32).view(np.uint32)
+        n = int(np.count_nonzero(a != r))
+        if n:
+            bad[k] = (n, rel_l1(out[k], ref[k]))
+    assert bad == {}
+
+
+@pytest.mark.parametrize("case", ["W", "M", "seed1"])
+def test_bitwise_fp32_scenarios(lib, ds, scenarios, oracle_mod, case):
+    import make_fixtures as mf
+    s = mf.perturbed(ds, 1) if case == "seed1" else scenarios[case]
+    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=ca.VARIANT_KCACHE)
+    ref = oracle_outputs(oracle_mod, s, 300, 64, precision=ca.FP32)
+    for _, k in ca.VALIDATED:
+        a = np.ascontiguousarray(out[k], dtype=np.float32).view(np.uint32)
+        r = np.ascontiguousarray(ref[k], dtype=np.float32).view(np.uint32)
+        assert np.array_equal(a, r), (k, int(np.count_nonzero(a != r)))

@@ -54,5 +54,17 @@ for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,3,4").spl
                                   for d in segd],
            "wait_frac_of_busy": round(float(wait.sum() / dur.sum()), 4),
            "seg_wait_us_mean": [round(float(wait[s * nb:(s + 1) * nb].mean()), 1) for s in range(nseg)]}
+    # concurrency timeline: mean number of running items in 20 equal time bins,
+    # and the mean duration of the items that START in each bin (per segment)
+    edges = np.linspace(0.0, makespan, 21)
+    active = []
+    for a, b in zip(edges[:-1], edges[1:]):
+        ov = np.clip(np.minimum(en, b) - np.maximum(st, a), 0.0, None)
+        active.append(round(float(ov.sum() / (b - a)), 1))
+    out["active_items_per_bin"] = active
+    out["first_drop_below_full_us"] = round(float(le[0]), 1)
+    sbin = np.clip(np.digitize(st, edges) - 1, 0, 19)
+    out["dur_us_by_start_bin"] = [round(float(dur[sbin == i].mean()), 1) if np.any(sbin == i) else None
+                                  for i in range(20)]
     print(json.dumps(out), flush=True)
 g.close()

@@ -20,6 +20,14 @@ struct HostCold {
   double exp(double x) const { return cloudsc_libm::exp(x, HostTabs{}); }
   double pow(double x, double y) const { return cloudsc_libm::pow(x, y, HostTabs{}); }
 };
+struct HostColdF {
+  float expf(float x) const { return cloudsc_libm::expf(x, cloudsc_libm::HostTabsF{}); }
+  float powf(float x, float y) const { return cloudsc_libm::powf(x, y, cloudsc_libm::HostTabsF{}); }
+};
+static float split_expf(float x) { return cloudsc_libm::expf_split(x, cloudsc_libm::HostTabsF{}, HostColdF{}); }
+static float split_powf(float x, float y) {
+  return cloudsc_libm::powf_split(x, y, cloudsc_libm::HostTabsF{}, HostColdF{});
+}
 static double split_exp(double x) { return cloudsc_libm::exp_split(x, HostTabs{}, HostCold{}); }
 static double split_pow(double x, double y) { return cloudsc_libm::pow_split(x, y, HostTabs{}, HostCold{}); }
 
@@ -36,6 +44,13 @@ struct Tally {
   const char* name;
   long long n = 0, bad = 0, worst = 0;
   double bx = 0, by = 0;
+  void addf(float got, float want, float x, float y) {
+    ++n;
+    if (std::memcmp(&got, &want, 4) != 0 && !(std::isnan(got) && std::isnan(want))) {
+      if (bad++ < 3) std::fprintf(stderr, "  %s(%a, %a): got %a want %a\n", name, x, y, got, want);
+      worst = 1;
+    }
+  }
   void add(double got, double want, double x, double y) {
     ++n;
     if (std::memcmp(&got, &want, 8) != 0 && !(std::isnan(got) && std::isnan(want))) {
@@ -146,6 +161,55 @@ int main(int argc, char** argv) {
       t.add(cloudsc_libm::pow(p[0], p[1], tabs), std::pow(p[0], p[1]), p[0], p[1]);
       t.add(split_pow(p[0], p[1]), std::pow(p[0], p[1]), p[0], p[1]);
     }
+    fail |= t.report();
+  }
+  // ---------------- single precision ----------------
+  cloudsc_libm::HostTabsF tf;
+  std::uniform_real_distribution<float> uf(0.0f, 1.0f);
+  {
+    Tally t{"expf x in [-110,90]"};
+    for (long long s = 0; s < M; ++s) {
+      const float x = -110.0f + 200.0f * uf(rng);
+      t.addf(cloudsc_libm::expf(x, tf), ::expf(x), x, 0);
+      t.addf(split_expf(x), ::expf(x), x, 0);
+    }
+    fail |= t.report();
+  }
+  {
+    Tally t{"expf bit patterns (stride)"};
+    for (uint64_t b = 0; b < (1ULL << 32); b += (M < 4000000 ? 128 : 8) + (rng() & 7)) {
+      float x;
+      const uint32_t u = (uint32_t)b;
+      std::memcpy(&x, &u, 4);
+      t.addf(cloudsc_libm::expf(x, tf), ::expf(x), x, 0);
+    }
+    fail |= t.report();
+  }
+  {
+    const float ys[] = {0.666f, 1.5f, 0.333f, 0.4f, 0.5777f, 3.0f, 2.47f, -1.79f, 1.15f, -0.3f, 0.25f, 0.11f, 0.5f};
+    Tally t{"powf kernel exponents"};
+    for (long long s = 0; s < M; ++s) {
+      const float x = std::exp2(-60.0f + 80.0f * uf(rng));
+      const float y = ys[s % (sizeof(ys) / sizeof(ys[0]))];
+      t.addf(cloudsc_libm::powf(x, y, tf), ::powf(x, y), x, y);
+      t.addf(split_powf(x, y), ::powf(x, y), x, y);
+    }
+    fail |= t.report();
+  }
+  {
+    Tally t{"powf random bits"};
+    for (long long s = 0; s < M; ++s) {
+      uint32_t bx = (uint32_t)rng(), by = (uint32_t)rng();
+      float x, y;
+      std::memcpy(&x, &bx, 4);
+      std::memcpy(&y, &by, 4);
+      if (s & 1) y = std::ldexp(y, -(int)(by % 120));
+      t.addf(cloudsc_libm::powf(x, y, tf), ::powf(x, y), x, y);
+      t.addf(split_powf(x, y), ::powf(x, y), x, y);
+    }
+    const float sp[][2] = {{0.0f, 0.666f}, {0.0f, -1.0f}, {-0.0f, 3.0f}, {-2.0f, 3.0f}, {-2.0f, 0.5f}, {1.0f, NAN},
+                           {NAN, 0.0f}, {INFINITY, 0.5f}, {1e-40f, 0.666f}, {2.0f, 200.0f}, {2.0f, -149.5f}};
+    for (auto& p : sp) t.addf(cloudsc_libm::powf(p[0], p[1], tf), ::powf(p[0], p[1]), p[0], p[1]);
     fail |= t.report();
   }
   return fail;
