@@ -33,8 +33,8 @@ HBM_PEAK_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.m
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)    # 0.2 s of kernels: a stable mean
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--ngptot", type=int, default=163840, help="columns per GPU")
     p.add_argument("--nproma", type=int, default=64,
                    help="NPROMA (block = workgroup); 64 is the measured best for the persistent kernel "

@@ -808,7 +808,8 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       qn_s = qn_s - u_ls * qn_l;
       qn_s = qn_s - u_is * qn_i;
       // back substitution (step 2): vapour and the diagonal solves
-      qn_v = cl_div(qn_v, R(1.0));
+      // qn_v = qn_v / zqlhs[qv][qv] with a pivot of exactly 1: x / 1 == x in IEEE arithmetic
+      // (signed zeros and NaN included), so the division is dropped
       qn_s = cl_div(qn_s, d_s);
       qn_r = cl_div(qn_r, d_r);
       qn_i = cl_div(qn_i, d_i);
