@@ -522,3 +522,11 @@ def test_bitwise_fp32_scenarios(lib, ds, scenarios, oracle_mod, case):
         a = np.ascontiguousarray(out[k], dtype=np.float32).view(np.uint32)
         r = np.ascontiguousarray(ref[k], dtype=np.float32).view(np.uint32)
         assert np.array_equal(a, r), (k, int(np.count_nonzero(a != r)))
+
+
+def test_bitwise_full_size_vs_oracle(lib, ds, oracle_mod):
+    """BASELINE size (163840 columns, NPROMA 64) with the bench's default kernel
+    (KSEG): every validated field bit-identical to the oracle run at full size."""
+    out = run_gpu(ds, 163840, 64, variant=ca.VARIANT_KSEG)
+    ref = oracle_outputs(oracle_mod, ds, 163840, 64)
+    assert bitwise_mismatches(out, ref) == {}
