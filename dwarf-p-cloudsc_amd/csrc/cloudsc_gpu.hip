@@ -186,7 +186,10 @@ namespace {
 
 template <typename real> int kcache_default_cfg();
 template <> int kcache_default_cfg<double>() { return 20; }    // 2 waves/SIMD, carried state in registers
-template <> int kcache_default_cfg<float>() { return 140; }   // 4 waves/SIMD, carried state in LDS
+// fp32 KCACHE: 3 waves/SIMD with the register prefetch of level k+1; with the
+// double-internal expf/powf it is 2-3 % faster than the 4-wave LDS-carry cfg 140
+// (profiles/r01/sweep_fp32_cfgs_libm.jsonl)
+template <> int kcache_default_cfg<float>() { return 31; }
 template <typename real> int kseg_default_cfg();
 // fp64 KSEG: 2 waves/SIMD, carried state in LDS, neighbour levels re-read (cfg
 // 122): with the LDS-table exp/pow it is 5-7 % faster than the register-carry
