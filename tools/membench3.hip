@@ -9,7 +9,7 @@
 // fp64 workload: `ilp` independent chains of `len` dependent FMAs each, seeded
 // by the level's loads, feeding the level's stores.
 //
-//   ./membench3 <len> <ilp> [ngptot] [mode: 0 = persistent, 1 = one-shot grid]
+//   ./membench3 <len> <ilp> [ngptot] [mode: 0 = persistent, 1 = one-shot grid] [waves per SIMD: 2]
 // prints one JSON line: ms, algorithmic TB/s, FMAs per wave-level.
 //
 // build: hipcc --offload-arch=gfx950 -O3 tools/membench3.hip -o build/membench3
@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(64) oneshot(Ptrs p, int klev, int len) {
 }
 
 template <int ILP>
-float run(Ptrs p, int klev, int nblocks, unsigned* counter, int len, int mode, size_t lds) {
+float run(Ptrs p, int klev, int nblocks, unsigned* counter, int len, int mode, size_t lds, int grid) {
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
@@ -96,7 +96,7 @@ float run(Ptrs p, int klev, int nblocks, unsigned* counter, int len, int mode, s
     CHK(hipMemset(counter, 0, 4));
     CHK(hipEventRecord(a));
     if (mode == 0)
-      hipLaunchKernelGGL(persistent<ILP>, dim3(2048), dim3(64), lds, 0, p, klev, nblocks, counter, len);
+      hipLaunchKernelGGL(persistent<ILP>, dim3(grid), dim3(64), lds, 0, p, klev, nblocks, counter, len);
     else
       hipLaunchKernelGGL(oneshot<ILP>, dim3(nblocks), dim3(64), lds, 0, p, klev, len);
     CHK(hipEventRecord(b));
@@ -113,6 +113,7 @@ int main(int argc, char** argv) {
   const int ilp = argc > 2 ? atoi(argv[2]) : 1;
   const int ngptot = argc > 3 ? atoi(argv[3]) : 163840;
   const int mode = argc > 4 ? atoi(argv[4]) : 0;
+  const int wps = argc > 5 ? atoi(argv[5]) : 2;   // waves per SIMD (LDS-capped residency)
   const int klev = 137, nblocks = ngptot / 64;
   const size_t plane = (size_t)nblocks * klev * 64;
   Ptrs p;
@@ -127,19 +128,20 @@ int main(int argc, char** argv) {
   }
   unsigned* counter;
   CHK(hipMalloc(&counter, 4));
-  // 20 KB of dynamic LDS per workgroup: 8 one-wave workgroups per CU = 2 waves per SIMD
-  const size_t lds = 20 * 1024;
+  // dynamic LDS per one-wave workgroup: 160 KB / (4 SIMDs * wps) caps residency at wps waves per SIMD
+  const size_t lds = (160 * 1024) / (4 * wps) - 512;
+  const int grid = 256 * 4 * wps;
   float ms = 0.0f;
   switch (ilp) {
-    case 1: ms = run<1>(p, klev, nblocks, counter, len, mode, lds); break;
-    case 2: ms = run<2>(p, klev, nblocks, counter, len, mode, lds); break;
-    case 4: ms = run<4>(p, klev, nblocks, counter, len, mode, lds); break;
-    case 8: ms = run<8>(p, klev, nblocks, counter, len, mode, lds); break;
+    case 1: ms = run<1>(p, klev, nblocks, counter, len, mode, lds, grid); break;
+    case 2: ms = run<2>(p, klev, nblocks, counter, len, mode, lds, grid); break;
+    case 4: ms = run<4>(p, klev, nblocks, counter, len, mode, lds, grid); break;
+    case 8: ms = run<8>(p, klev, nblocks, counter, len, mode, lds, grid); break;
     default: printf("ilp must be 1, 2, 4 or 8\n"); return 1;
   }
   const double bytes = (double)ngptot * klev * (NIN + NOUT) * 8.0;
-  printf("{\"len\": %d, \"ilp\": %d, \"mode\": \"%s\", \"fma_per_wave_level\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", len,
-         ilp, mode == 0 ? "persistent" : "oneshot", len * ilp, ms, bytes / (ms * 1e-3) / 1e12);
+  printf("{\"len\": %d, \"ilp\": %d, \"mode\": \"%s\", \"waves_per_simd\": %d, \"fma_per_wave_level\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n",
+         len, ilp, mode == 0 ? "persistent" : "oneshot", wps, len * ilp, ms, bytes / (ms * 1e-3) / 1e12);
   for (double* d : bufs) CHK(hipFree(d));
   CHK(hipFree(counter));
   return 0;
