@@ -220,25 +220,32 @@ int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma,
 }
 
 // ---- persistent segmented variant ----
-// workspace: [counter, err, pad..][flags: nblocks][carry state], 256-byte aligned parts
+// Every item is one wave: a block of NPROMA > 64 columns is run as
+// ceil(NPROMA/64) 64-column sub-blocks (the block layout is unchanged: sub-block
+// h is columns h*64.. of each plane of the block), so every NPROMA runs with the
+// one-wave schedule that measures fastest (profiles/r01/nproma_sweep_*).
+int kseg_nsub(int nproma) { return (nproma + 63) / 64; }
+int kseg_wg(int nproma) { return nproma < 64 ? nproma : 64; }
+// workspace: [counter, err, pad..][flags: nblocks*nsub][carry state], 256-byte aligned parts
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-size_t kseg_ctl_bytes(int nblocks) { return align256(256 + (size_t)nblocks * sizeof(unsigned)); }
+size_t kseg_ctl_bytes(int nblocks, int nproma) {
+  return align256(256 + (size_t)nblocks * kseg_nsub(nproma) * sizeof(unsigned));
+}
 template <typename real>
 size_t kseg_scratch_bytes(int nblocks, int nproma) {
-  return kseg_ctl_bytes(nblocks) + (size_t)nblocks * kCarryN * nproma * sizeof(real);
+  return kseg_ctl_bytes(nblocks, nproma) + (size_t)nblocks * kCarryN * nproma * sizeof(real);
 }
 
 // Segmentation, measured (profiles/r01/kseg_nseg_sweep*.jsonl,
-// kseg_bounds_sweep_*.jsonl):
-//  - NPROMA > 64 (multi-wave workgroups, 1024 slots for 1280+ blocks): 8 even
-//    segments of the physics levels;
-//  - NPROMA <= 64 (one wave per workgroup, 2048 slots): 2 segments, the
-//    second one smaller ("guided": the items dequeued last are short, so the
-//    tail is short; lower levels also cost more per level) -- the split at
-//    NCLDTOP + 62 % of the physics levels; each hand-off costs 19 values out
-//    and in plus an L1 invalidate, so fewer segments win once the tail is short.
+// kseg_bounds_sweep_*.jsonl), for one-wave items (2048 slots): 2 segments, the
+// second one smaller ("guided": the items dequeued last are short, so the tail
+// is short; lower levels also cost more per level) -- the split at NCLDTOP +
+// 62 % of the physics levels; each hand-off costs 19 values out and in plus an
+// L1 invalidate, so fewer segments win once the tail is short.  (Multi-wave
+// workgroups, the earlier NPROMA > 64 form, wanted 8 even segments.)
 int kseg_nseg(int nproma) {
-  int n = nproma > 64 ? 8 : 2;
+  (void)nproma;
+  int n = 2;
   if (const char* e = getenv("CLOUDSC_KSEG_NSEG")) n = atoi(e);
   return n < 1 ? 1 : (n > kMaxSeg ? kMaxSeg : n);
 }
@@ -247,7 +254,8 @@ void kseg_bounds(int nseg, int klev, int ncldtop, int nproma, int* lev) {
   const int top = ncldtop - 1 < klev ? (ncldtop - 1 > 0 ? ncldtop - 1 : 0) : klev;
   const int phys = klev - top;
   lev[0] = 0;
-  if (nseg == 2 && nproma <= 64) {
+  (void)nproma;
+  if (nseg == 2) {
     lev[1] = top + (int)((62LL * phys + 50) / 100);
     if (lev[1] <= 0) lev[1] = 1;
     if (lev[1] >= klev) lev[1] = klev - 1;
@@ -260,17 +268,18 @@ void kseg_bounds(int nseg, int klev, int ncldtop, int nproma, int* lev) {
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
   auto kern = kseg_entry<real, WAVES, PF, AER, LDSC>;
-  const size_t lds = LDSC ? carry_lds_bytes<real>(nproma) : 0;
+  const int wg = kseg_wg(nproma);
+  const size_t lds = LDSC ? carry_lds_bytes<real>(wg) : 0;
   // one workgroup per resident slot (an over-estimate only delays the extra
   // workgroups: progress never depends on residency, items are dequeued in order).
-  // Cached per NPROMA; threads driving different devices may race here, hence atomics.
-  static std::atomic<int> cache[257];
-  int per_cu = cache[nproma].load(std::memory_order_relaxed);
+  // Cached per workgroup size; threads driving different devices may race here, hence atomics.
+  static std::atomic<int> cache[65];
+  int per_cu = cache[wg].load(std::memory_order_relaxed);
   if (!per_cu) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, nproma, lds) != hipSuccess || n <= 0) n = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, wg, lds) != hipSuccess || n <= 0) n = 1;
     per_cu = n;
-    cache[nproma].store(n, std::memory_order_relaxed);
+    cache[wg].store(n, std::memory_order_relaxed);
   }
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -279,7 +288,7 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   int grid = per_cu * ncu;
   if (const char* e = getenv("CLOUDSC_KSEG_GRID")) grid = atoi(e) > 0 ? atoi(e) : grid;
   if (grid > nitems) grid = nitems;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(nproma), lds, st, a, pa);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, st, a, pa);
   return CLOUDSC_OK;
 }
 
@@ -320,11 +329,17 @@ int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, i
     pa.counter = (unsigned*)scratch;
     pa.err = (unsigned*)scratch + 1;
     pa.flags = (unsigned*)((char*)scratch + 256);
-    pa.state = (real*)((char*)scratch + kseg_ctl_bytes(nblocks));
+    pa.state = (real*)((char*)scratch + kseg_ctl_bytes(nblocks, nproma));
+    pa.nsub = kseg_nsub(nproma);
+    // item order (segment, block, sub-block); CLOUDSC_KSEG_SBMAJOR=1 runs
+    // (segment, sub-block, block) instead -- the same within noise at NPROMA 128,
+    // 2 % slower at 256 (profiles/r01/kseg_subblock_order.jsonl)
+    pa.sb_major = 0;
+    if (const char* e = getenv("CLOUDSC_KSEG_SBMAJOR")) pa.sb_major = atoi(e) != 0;
     pa.nseg = kseg_nseg(nproma);
     if (pa.nseg > klev) pa.nseg = klev;
     pa.nblocks = nblocks;
-    pa.nitems = pa.nseg * nblocks;
+    pa.nitems = pa.nseg * nblocks * pa.nsub;
     for (int q = 0; q <= kMaxSeg; q++) pa.lev[q] = klev;
     kseg_bounds(pa.nseg, klev, ncldtop, nproma, pa.lev);
     if (const char* e = getenv("CLOUDSC_KSEG_BOUNDS")) {   // experiments: explicit interior boundaries
@@ -338,9 +353,9 @@ int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, i
       }
       pa.nseg = n;
       pa.lev[n] = klev;
-      pa.nitems = pa.nseg * nblocks;
+      pa.nitems = pa.nseg * nblocks * pa.nsub;
     }
-    HIPCHK(hipMemsetAsync(scratch, 0, kseg_ctl_bytes(nblocks), st));
+    HIPCHK(hipMemsetAsync(scratch, 0, kseg_ctl_bytes(nblocks, nproma), st));
     rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, cfg)
              : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, cfg);
   } else {

@@ -1085,10 +1085,12 @@ __device__ unsigned long long g_kseg_trace[4 * kTraceMax];
 template <typename real>
 struct PersistArgs {
   unsigned* counter;      // dequeue counter (zeroed per launch)
-  unsigned* flags;        // [nblocks] segments completed (zeroed per launch)
+  unsigned* flags;        // [nblocks * nsub] segments completed (zeroed per launch)
   unsigned* err;          // spin-limit violations (zeroed per launch)
   real* state;            // [nblocks][kCarryN][nproma]
   int nseg, nitems, nblocks;
+  int nsub;               // 64-column sub-blocks per NPROMA block (one wave each)
+  int sb_major;           // item order (segment, sub-block, block) instead of (segment, block, sub-block)
   int lev[kMaxSeg + 1];
 };
 
@@ -1124,8 +1126,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
                                                                const PersistArgs<real>& P) {
   __shared__ int s_item;
   const KArgs<real>& A = *(const KArgs<real>*)ka;
-  const int nproma = A.nproma, jl = threadIdx.x;
-  const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
+  const int nproma = A.nproma, nsub = P.nsub;
   // Every branch around a barrier is wave-uniform, and visibly so to the
   // compiler (SGPR conditions): the first wave of the workgroup does the
   // dequeue, the polling and the flag store with all of its lanes (same address,
@@ -1133,7 +1134,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
   // inside this loop gets restructured into nested exec-masked loops whose
   // barriers no longer pair up across waves.
   const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;
-  const unsigned one = jl == 0 ? 1u : 0u;           // lane 0 counts, the others add 0
+  const unsigned one = threadIdx.x == 0 ? 1u : 0u;  // lane 0 counts, the others add 0
   for (;;) {
     if (wave0) {
       const unsigned old = __hip_atomic_fetch_add(P.counter, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1143,7 +1144,15 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
     const int item = __builtin_amdgcn_readfirstlane(s_item);
     __syncthreads();                                   // s_item is rewritten next iteration
     if (item >= P.nitems) break;
-    const int seg = item / P.nblocks, b = item - seg * P.nblocks;
+    // item = (segment, block b, 64-column sub-block h), segment-major (or
+    // (segment, h, b) with sb_major): a block of NPROMA > 64 columns is run
+    // as nsub one-wave items over the same block layout (sub-block h is the 64
+    // contiguous columns h*64.. of each plane); flags are per (b, h)
+    const int nsb = P.nblocks * nsub;
+    const int seg = item / nsb, sb = item - seg * nsb;
+    const int b = P.sb_major ? sb % P.nblocks : sb / nsub;
+    const int jl = (P.sb_major ? sb / P.nblocks : sb - b * nsub) * 64 + (int)threadIdx.x;
+    const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
 #ifdef CLOUDSC_KSEG_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_ready = t_start;
@@ -1163,7 +1172,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       if (wave0) {
         for (unsigned spins = 0;; spins++) {
           const unsigned f = __builtin_amdgcn_readfirstlane(
-              __hip_atomic_load(P.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+              __hip_atomic_load(P.flags + sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
           if (f >= (unsigned)seg) break;
           if (spins > (1u << 24)) {                      // bounded: never hang
             __hip_atomic_fetch_add(P.err, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1189,12 +1198,12 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, true);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (wave0) __hip_atomic_store(P.flags + b, (unsigned)(seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (wave0) __hip_atomic_store(P.flags + sb, (unsigned)(seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (active) {
       stg(((const KArgs<real>*)launder_uniform(ka))->prainfrac, (size_t)b * nproma, lo, cs.rainfrac);
     }
 #ifdef CLOUDSC_KSEG_TRACE
-    if (jl == 0 && item < kTraceMax) {   // diagnostic build only: schedule of every item
+    if (threadIdx.x == 0 && item < kTraceMax) {   // diagnostic build only: schedule of every item
       g_kseg_trace[4 * item + 0] = t_start;
       g_kseg_trace[4 * item + 1] = __builtin_amdgcn_s_memrealtime();
       g_kseg_trace[4 * item + 2] = blockIdx.x;

@@ -21,7 +21,7 @@ lib.cloudsc_kseg_trace.argtypes = [C.c_void_p, C.c_int]
 ds = ca.load_dataset()
 prec = ca.FP64 if (len(sys.argv) < 2 or sys.argv[1] == "fp64") else ca.FP32
 ngptot, nproma = 163840, int(os.environ.get("TRACE_NPROMA", "64"))
-nb = ngptot // nproma
+nb = (ngptot // nproma) * ((nproma + 63) // 64)   # one-wave items: 64-column sub-blocks
 g = ca.GpuState(ds, ngptot, nproma, prec)
 for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,3,4").split(",")]:
     os.environ["CLOUDSC_KSEG_NSEG"] = str(nseg)
