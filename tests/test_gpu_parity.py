@@ -432,8 +432,10 @@ def bitwise_mismatches(out, ref):
 
 
 @pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
-@pytest.mark.parametrize("ngptot,nproma", [(100, 128), (1000, 128), (1000, 64)])
+@pytest.mark.parametrize("ngptot,nproma", [(100, 128), (1000, 128), (1000, 64), (1000, 100), (1000, 256)])
 def test_bitwise_vs_oracle(lib, ds, oracle_mod, variant, ngptot, nproma):
+    # NPROMA 100 / 128 / 256: KSEG runs each block as 64-column one-wave items
+    # (the last one of a block partial at NPROMA 100)
     out = run_gpu(ds, ngptot, nproma, variant=variant)
     ref = oracle_outputs(oracle_mod, ds, ngptot, nproma)
     assert bitwise_mismatches(out, ref) == {}
