@@ -69,9 +69,33 @@ template <typename T>
 __device__ __forceinline__ T ldg(const T* ubase, size_t uidx, unsigned lane_bytes) {
   return *(const T*)((const char*)(ubase + uidx) + lane_bytes);
 }
+// Outputs are written once and never read back by the kernel, and the level
+// inputs are read once: both go as non-temporal (streaming) accesses, so the
+// caches keep what is re-read (the neighbour levels, the hand-off state).
+// -1.9 % kernel time on the same box (profiles/r01/ab_nontemporal.txt);
+// CLOUDSC_CACHED_IO restores plain accesses.  stg_cached is for scratch that
+// is read back (the SCC variant's temporaries).
+template <typename T>
+__device__ __forceinline__ void stg_cached(T* ubase, size_t uidx, unsigned lane_bytes,
+                                           typename std::common_type<T>::type v) {
+  *(T*)((char*)(ubase + uidx) + lane_bytes) = v;
+}
 template <typename T>
 __device__ __forceinline__ void stg(T* ubase, size_t uidx, unsigned lane_bytes, typename std::common_type<T>::type v) {
-  *(T*)((char*)(ubase + uidx) + lane_bytes) = v;
+#ifndef CLOUDSC_CACHED_IO
+  __builtin_nontemporal_store(v, (T*)((char*)(ubase + uidx) + lane_bytes));
+#else
+  stg_cached(ubase, uidx, lane_bytes, v);
+#endif
+}
+// a level input, read exactly once
+template <typename T>
+__device__ __forceinline__ T ldg1(const T* ubase, size_t uidx, unsigned lane_bytes) {
+#ifndef CLOUDSC_CACHED_IO
+  return __builtin_nontemporal_load((const T*)((const char*)(ubase + uidx) + lane_bytes));
+#else
+  return ldg(ubase, uidx, lane_bytes);
+#endif
 }
 
 // Per-level inputs of one column (the prefetch unit).
@@ -170,19 +194,19 @@ template <typename real, bool AER>
 __device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& A, size_t u2, size_t u3, int k,
                                            int klev, int nproma, unsigned lo) {
   const size_t i = u2 + (size_t)k * nproma;
-  L.pt = ldg(A.pt, i, lo); L.pq = ldg(A.pq, i, lo); L.ttt = ldg(A.ttt, i, lo); L.ttq = ldg(A.ttq, i, lo);
-  L.tta = ldg(A.tta, i, lo); L.pa = ldg(A.pa, i, lo); L.pap = ldg(A.pap, i, lo);
-  L.plude = ldg(A.plude_in, i, lo); L.pvfl = ldg(A.pvfl, i, lo); L.pvfi = ldg(A.pvfi, i, lo);
+  L.pt = ldg1(A.pt, i, lo); L.pq = ldg1(A.pq, i, lo); L.ttt = ldg1(A.ttt, i, lo); L.ttq = ldg1(A.ttq, i, lo);
+  L.tta = ldg1(A.tta, i, lo); L.pa = ldg1(A.pa, i, lo); L.pap = ldg1(A.pap, i, lo);
+  L.plude = ldg1(A.plude_in, i, lo); L.pvfl = ldg1(A.pvfl, i, lo); L.pvfi = ldg1(A.pvfi, i, lo);
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const size_t j = u3 + ((size_t)m * klev + k) * nproma;
-    L.pclv[m] = ldg(A.pclv, j, lo);
-    L.ttcld[m] = ldg(A.ttcld, j, lo);
+    L.pclv[m] = ldg1(A.pclv, j, lo);
+    L.ttcld[m] = ldg1(A.ttcld, j, lo);
   }
-  L.phrsw = ldg(A.phrsw, i, lo); L.phrlw = ldg(A.phrlw, i, lo); L.pvervel = ldg(A.pvervel, i, lo);
-  L.psnde = ldg(A.psnde, i, lo); L.psupsat = ldg(A.psupsat, i, lo);
+  L.phrsw = ldg1(A.phrsw, i, lo); L.phrlw = ldg1(A.phrlw, i, lo); L.pvervel = ldg1(A.pvervel, i, lo);
+  L.psnde = ldg1(A.psnde, i, lo); L.psupsat = ldg1(A.psupsat, i, lo);
   if (AER) {   // LAERICESED / LAERICEAUTO inputs; the launch picks AER from the flags
-    L.pre_ice = ldg(A.pre_ice, i, lo); L.picrit_aer = ldg(A.picrit_aer, i, lo); L.pnice = ldg(A.pnice, i, lo);
+    L.pre_ice = ldg1(A.pre_ice, i, lo); L.picrit_aer = ldg1(A.picrit_aer, i, lo); L.pnice = ldg1(A.pnice, i, lo);
   } else {
     L.pre_ice = R(0.0); L.picrit_aer = R(1.0); L.pnice = R(1.0);
   }

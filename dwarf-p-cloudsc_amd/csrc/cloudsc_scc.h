@@ -43,15 +43,15 @@ inline SccScratch<real> scc_scratch_carve(char* base, long long nblocks, long lo
 
 template <typename real>
 __device__ __forceinline__ void scc_put_ls(real* base, size_t idx, size_t plane, unsigned lo, const LevelState<real>& s) {
-  stg(base, idx + 0 * plane, lo, s.ztp1); stg(base, idx + 1 * plane, lo, s.za);
-  stg(base, idx + 2 * plane, lo, s.zaorig); stg(base, idx + 3 * plane, lo, s.zfoealfa);
-  stg(base, idx + 4 * plane, lo, s.ttend); stg(base, idx + 5 * plane, lo, s.qtend);
+  stg_cached(base, idx + 0 * plane, lo, s.ztp1); stg_cached(base, idx + 1 * plane, lo, s.za);
+  stg_cached(base, idx + 2 * plane, lo, s.zaorig); stg_cached(base, idx + 3 * plane, lo, s.zfoealfa);
+  stg_cached(base, idx + 4 * plane, lo, s.ttend); stg_cached(base, idx + 5 * plane, lo, s.qtend);
 #pragma unroll
-  for (int m = 0; m < 5; m++) stg(base, idx + (6 + m) * plane, lo, s.zqx[m]);
+  for (int m = 0; m < 5; m++) stg_cached(base, idx + (6 + m) * plane, lo, s.zqx[m]);
 #pragma unroll
-  for (int m = 0; m < 4; m++) stg(base, idx + (11 + m) * plane, lo, s.zqx0[m]);
+  for (int m = 0; m < 4; m++) stg_cached(base, idx + (11 + m) * plane, lo, s.zqx0[m]);
 #pragma unroll
-  for (int m = 0; m < 4; m++) stg(base, idx + (15 + m) * plane, lo, s.zlneg[m]);
+  for (int m = 0; m < 4; m++) stg_cached(base, idx + (15 + m) * plane, lo, s.zlneg[m]);
 }
 template <typename real>
 __device__ __forceinline__ void scc_get_ls(const real* base, size_t idx, size_t plane, unsigned lo, LevelState<real>& s) {
@@ -102,7 +102,7 @@ __device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const Scc
   CarryState<real> cs;
   init_carry<real>(cs);
 #pragma unroll
-  for (int m = 0; m < 3; m++) stg(S.pfx, upfb + (size_t)m * pstride, lo, R(0.0));   // zpfplsx(:,1) = 0
+  for (int m = 0; m < 3; m++) stg_cached(S.pfx, upfb + (size_t)m * pstride, lo, R(0.0));   // zpfplsx(:,1) = 0
   for (int k = 0; k < klev; k++) {
     const bool physics = k >= ncldtop0;
     const KArgs<real>& A = SCC_A;
@@ -133,10 +133,10 @@ __device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const Scc
     if (physics) physics_level(SCC_C, k, klev, ncldtop0, in, nb, cc, ls, cs, po);
     store_level(SCC_A, u2, u3, k, klev, nproma, lo, physics, ls, po);
 #pragma unroll
-    for (int m = 0; m < 4; m++) stg(S.qxn, uqxb + (size_t)m * plane + (size_t)k * nproma, lo, po.zqxn[m]);
-    stg(S.pfx, upfb + 0 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_i);
-    stg(S.pfx, upfb + 1 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_r);
-    stg(S.pfx, upfb + 2 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_s);
+    for (int m = 0; m < 4; m++) stg_cached(S.qxn, uqxb + (size_t)m * plane + (size_t)k * nproma, lo, po.zqxn[m]);
+    stg_cached(S.pfx, upfb + 0 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_i);
+    stg_cached(S.pfx, upfb + 1 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_r);
+    stg_cached(S.pfx, upfb + 2 * pstride + (size_t)(k + 1) * nproma, lo, cs.pfx_s);
   }
   stg(SCC_A.prainfrac, u1, lo, cs.rainfrac);
 
