@@ -240,7 +240,8 @@ size_t kseg_scratch_bytes(int nblocks, int nproma) {
 // kseg_bounds_sweep_*.jsonl), for one-wave items (2048 slots): 2 segments, the
 // second one smaller ("guided": the items dequeued last are short, so the tail
 // is short; lower levels also cost more per level) -- the split at NCLDTOP +
-// 62 % of the physics levels; each hand-off costs 19 values out and in plus an
+// 60 % of the physics levels (re-tuned with the streaming I/O: 1.768 ms against
+// 1.788 at 62 %, profiles/r01/kseg_bounds_sweep_nt.jsonl); each hand-off costs 19 values out and in plus an
 // L1 invalidate, so fewer segments win once the tail is short.  (Multi-wave
 // workgroups, the earlier NPROMA > 64 form, wanted 8 even segments.)
 int kseg_nseg(int nproma) {
@@ -256,7 +257,7 @@ void kseg_bounds(int nseg, int klev, int ncldtop, int nproma, int* lev) {
   lev[0] = 0;
   (void)nproma;
   if (nseg == 2) {
-    lev[1] = top + (int)((62LL * phys + 50) / 100);
+    lev[1] = top + (int)((60LL * phys + 50) / 100);
     if (lev[1] <= 0) lev[1] = 1;
     if (lev[1] >= klev) lev[1] = klev - 1;
   } else {
