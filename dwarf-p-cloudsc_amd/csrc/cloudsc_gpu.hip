@@ -191,10 +191,11 @@ template <> int kcache_default_cfg<double>() { return 20; }    // 2 waves/SIMD, 
 // (profiles/r01/sweep_fp32_cfgs_libm.jsonl)
 template <> int kcache_default_cfg<float>() { return 31; }
 template <typename real> int kseg_default_cfg();
-// fp64 KSEG: 2 waves/SIMD, carried state in LDS, neighbour levels re-read (cfg
-// 122): with the LDS-table exp/pow it is 5-7 % faster than the register-carry
-// cfg 20 (profiles/r01/sweep_kseg_ldsc_libm.jsonl)
-template <> int kseg_default_cfg<double>() { return 122; }
+// fp64 KSEG: 2 waves/SIMD, carried state and neighbour planes in registers
+// (cfg 20).  With the streaming I/O it is 1.8 % faster than the LDS-carry cfg
+// 122 (profiles/r01/sweep_kseg_cfgs_nt.jsonl), which had been 5-7 % faster
+// before it (sweep_kseg_ldsc_libm.jsonl).
+template <> int kseg_default_cfg<double>() { return 20; }
 template <> int kseg_default_cfg<float>() { return 31; }      // 3 waves/SIMD, register prefetch
 
 
