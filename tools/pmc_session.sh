@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 counter passes for one kernel configuration (each pass its own run,
 # --pmc with --kernel-trace only).  usage: tools/pmc_session.sh <tag> <prof_kernel.py args...>
+# PMC_PREC=F32 counts the fp32 VALU instruction classes instead of the fp64 ones.
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -12,7 +13,7 @@ passes=(
  "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_TC_INST_REQ"
  "FETCH_SIZE"
  "WRITE_SIZE"
- "SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_SALU SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64"
+ "SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_SALU SQ_INSTS_VALU_TRANS_${PMC_PREC:-F64} SQ_INSTS_VALU_FMA_${PMC_PREC:-F64} SQ_INSTS_VALU_MUL_${PMC_PREC:-F64} SQ_INSTS_VALU_ADD_${PMC_PREC:-F64}"
  "GRBM_GUI_ACTIVE GRBM_COUNT TCC_HIT_sum TCC_MISS_sum"
 )
 i=0
