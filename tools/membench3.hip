@@ -10,6 +10,7 @@
 // by the level's loads, feeding the level's stores.
 //
 //   ./membench3 <len> <ilp> [ngptot] [mode: 0 = persistent, 1 = one-shot grid] [waves per SIMD: 2]
+// mode 2 = persistent, two adjacent levels per load/store step (len ignored).
 // prints one JSON line: ms, algorithmic TB/s, FMAs per wave-level.
 //
 // build: hipcc --offload-arch=gfx950 -O3 tools/membench3.hip -o build/membench3
@@ -77,6 +78,41 @@ __global__ void __launch_bounds__(64) persistent(Ptrs p, int klev, int nblocks, 
   if (jl == 1000) pad[0] = 0.0;   // keeps the dynamic LDS allocation
 }
 
+// mode 2: the persistent schedule, but each step loads and stores two adjacent
+// levels together (1 KB contiguous per field and access pair instead of 512 B)
+__device__ __forceinline__ void level_pair(const Ptrs& p, size_t i, double& carry) {
+  double v[NIN], w[NIN];
+#pragma unroll
+  for (int f = 0; f < NIN; f++) { v[f] = p.in[f][i]; w[f] = p.in[f][i + 64]; }
+  double s = carry, t;
+#pragma unroll
+  for (int f = 0; f < NIN; f++) s += v[f];
+  t = s * 1e-3;
+#pragma unroll
+  for (int f = 0; f < NIN; f++) t += w[f];
+#pragma unroll
+  for (int f = 0; f < NOUT; f++) { p.out[f][i] = s + f; p.out[f][i + 64] = t + f; }
+  carry = t * 1e-3;
+}
+
+__global__ void __launch_bounds__(64) persistent_pair(Ptrs p, int klev, int nblocks, unsigned* counter) {
+  extern __shared__ double pad[];
+  __shared__ int s_item;
+  const int jl = threadIdx.x;
+  for (;;) {
+    if (jl == 0) s_item = (int)atomicAdd(counter, 1u);
+    __syncthreads();
+    const int b = s_item;
+    __syncthreads();
+    if (b >= nblocks) break;
+    double carry = 0.0;
+    int k = 0;
+    for (; k + 1 < klev; k += 2) level_pair(p, ((size_t)b * klev + k) * 64 + jl, carry);
+    if (k < klev) level<1>(p, ((size_t)b * klev + k) * 64 + jl, 0, carry);
+  }
+  if (jl == 1000) pad[0] = 0.0;
+}
+
 template <int ILP>
 __global__ void __launch_bounds__(64) oneshot(Ptrs p, int klev, int len) {
   extern __shared__ double pad[];
@@ -95,7 +131,9 @@ float run(Ptrs p, int klev, int nblocks, unsigned* counter, int len, int mode, s
   for (int rep = 0; rep < 6; rep++) {
     CHK(hipMemset(counter, 0, 4));
     CHK(hipEventRecord(a));
-    if (mode == 0)
+    if (mode == 2)
+      hipLaunchKernelGGL(persistent_pair, dim3(grid), dim3(64), lds, 0, p, klev, nblocks, counter);
+    else if (mode == 0)
       hipLaunchKernelGGL(persistent<ILP>, dim3(grid), dim3(64), lds, 0, p, klev, nblocks, counter, len);
     else
       hipLaunchKernelGGL(oneshot<ILP>, dim3(nblocks), dim3(64), lds, 0, p, klev, len);
@@ -141,7 +179,7 @@ int main(int argc, char** argv) {
   }
   const double bytes = (double)ngptot * klev * (NIN + NOUT) * 8.0;
   printf("{\"len\": %d, \"ilp\": %d, \"mode\": \"%s\", \"waves_per_simd\": %d, \"fma_per_wave_level\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n",
-         len, ilp, mode == 0 ? "persistent" : "oneshot", wps, len * ilp, ms, bytes / (ms * 1e-3) / 1e12);
+         len, ilp, mode == 0 ? "persistent" : (mode == 2 ? "persistent_pair" : "oneshot"), wps, len * ilp, ms, bytes / (ms * 1e-3) / 1e12);
   for (double* d : bufs) CHK(hipFree(d));
   CHK(hipFree(counter));
   return 0;
