@@ -428,7 +428,10 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
   if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return CLOUDSC_EINVAL;
   if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC && variant != CLOUDSC_VARIANT_KSEG)
     return CLOUDSC_EINVAL;
-  if (ngptot <= 0 || nproma <= 0 || nproma > 256 || klev < 2) return CLOUDSC_EINVAL;
+  // KCACHE and SCC run one workgroup of nproma threads per block; KSEG runs
+  // 64-column sub-blocks of any block width
+  const int max_nproma = variant == CLOUDSC_VARIANT_KSEG ? (1 << 24) : 256;
+  if (ngptot <= 0 || nproma <= 0 || nproma > max_nproma || klev < 2) return CLOUDSC_EINVAL;
   if (!g_inited[device]) return CLOUDSC_ENOINIT;
   return CLOUDSC_OK;
 }

@@ -144,7 +144,7 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
   *out = nullptr;
   int rc = cloudsc_gpu_init(device, params);
   if (rc) return rc;
-  rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KCACHE, ngptot, nproma, t->klev);
+  rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KSEG, ngptot, nproma, t->klev);
   if (rc) return rc;
   if (t->klon <= 0) return CLOUDSC_EINVAL;
   const void* req[] = {t->pt, t->pq, t->tendency_tmp_t, t->tendency_tmp_q, t->tendency_tmp_a,

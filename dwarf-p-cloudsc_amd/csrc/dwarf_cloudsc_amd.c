@@ -150,9 +150,12 @@ static int parse(int argc, char **argv, options_t *o) {
     o->numomp = (int)pos[0]; o->ngptot = (int)pos[1]; o->nproma = (int)pos[2];
     if (o->numomp <= 0) o->numomp = 1;
   }
-  if (o->ngptot <= 0 || o->nproma <= 0 || o->nproma > 256 || o->ngpus <= 0 || o->reps <= 0 || o->warmup < 0) {
-    fprintf(stderr, "invalid sizes: ngptot %d nproma %d (1..256) gpus %d reps %d\n", o->ngptot, o->nproma,
-            o->ngpus, o->reps);
+  /* KCACHE/SCC run one workgroup of NPROMA threads per block; KSEG any NPROMA */
+  const int max_nproma = o->variant == CLOUDSC_VARIANT_KSEG ? (1 << 24) : 256;
+  if (o->ngptot <= 0 || o->nproma <= 0 || o->nproma > max_nproma || o->ngpus <= 0 || o->reps <= 0 ||
+      o->warmup < 0) {
+    fprintf(stderr, "invalid sizes: ngptot %d nproma %d (1..%d) gpus %d reps %d\n", o->ngptot, o->nproma,
+            max_nproma, o->ngpus, o->reps);
     return -1;
   }
   return 0;

@@ -441,6 +441,30 @@ def test_bitwise_vs_oracle(lib, ds, oracle_mod, variant, ngptot, nproma):
     assert bitwise_mismatches(out, ref) == {}
 
 
+@pytest.mark.parametrize("ngptot,nproma", [(1000, 1000), (1000, 4096), (3000, 1000), (2048, 2048)])
+def test_bitwise_kseg_wide_blocks(lib, ds, oracle_mod, ngptot, nproma):
+    # KSEG accepts any NPROMA (KCACHE/SCC stop at 256 threads per block):
+    # blocks wider than the columns, ragged sub-blocks, a partial last block,
+    # and the level-major layout of a single block
+    out = run_gpu(ds, ngptot, nproma, variant=ca.VARIANT_KSEG)
+    ref = oracle_outputs(oracle_mod, ds, ngptot, nproma)
+    assert bitwise_mismatches(out, ref) == {}
+
+
+def test_wide_blocks_rejected_outside_kseg(lib, ds):
+    import ctypes as C
+    g = ca.GpuState(ds, 1024, 1024)
+    try:
+        f = ca.Fields()
+        ca.check(lib.cloudsc_state_fields(g.h, C.byref(f)))
+        for variant in (ca.VARIANT_KCACHE, ca.VARIANT_SCC):
+            assert lib.cloudsc_gpu_run(0, None, ca.FP64, variant, 1024, 1024, ds.klev, C.byref(f), None) == -1
+            assert lib.cloudsc_state_run(g.h, variant, 1, None) == -1
+        ca.check(lib.cloudsc_state_run(g.h, ca.VARIANT_KSEG, 1, None))
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("name", ["W", "M"])
 @pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG])
 def test_bitwise_vs_reference_kernel_scenarios(lib, scenarios, name, variant):

@@ -184,7 +184,8 @@ def test_cli_argument_errors():
         pytest.skip("dwarf-cloudsc-amd not built (needs libcloudsc_amd.so: __graft_entry__.build())")
     r = subprocess.run([DWARF, "1", "100"], capture_output=True, text=True)
     assert r.returncode == 1 and "right number of arguments" in r.stdout
-    r = subprocess.run([DWARF, "1", "100", "300"], capture_output=True, text=True)    # nproma > 256
+    # nproma > 256 with a one-workgroup-per-block variant (KSEG takes any NPROMA)
+    r = subprocess.run([DWARF, "--variant", "kcache", "1", "100", "300"], capture_output=True, text=True)
     assert r.returncode == 1 and "invalid sizes" in r.stderr
     r = subprocess.run([DWARF, "--variant", "nope"], capture_output=True, text=True)
     assert r.returncode == 1
