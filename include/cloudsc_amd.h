@@ -141,7 +141,10 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t *params);
  * SCC and KSEG need a workspace: pass scratch of cloudsc_gpu_scratch_bytes()
  * bytes (NULL is fine for KCACHE).  The KSEG workspace holds a dequeue counter
  * and per-block flags that are re-zeroed on `stream` before every launch, so one
- * workspace must not be shared by launches in flight on different streams. */
+ * workspace must not be shared by launches in flight on different streams.
+ * nproma: 1..256 for KCACHE and SCC (one workgroup of nproma threads per
+ * block), any positive value for KSEG (64-column sub-blocks); otherwise
+ * CLOUDSC_EINVAL. */
 int cloudsc_gpu_run(int device, void *stream, int precision, int variant,
                     int ngptot, int nproma, int klev,
                     const cloudsc_fields_t *device_fields, void *scratch);
