@@ -48,7 +48,9 @@ def parse():
                    help="also time the host-buffer path (H2D -> kernel -> D2H, chunked over streams): "
                         "reported as pcie_inclusive, never as value")
     p.add_argument("--transfer-steps", type=int, default=3)
-    p.add_argument("--cpu-sample", type=int, default=65536, help="columns in the CPU baseline sample")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="host threads of the CPU baseline (default: OMP_NUM_THREADS, else all host cores)")
+    p.add_argument("--no-hbm-peak", action="store_true", help="skip the in-run STREAM-copy measurement")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     a = p.parse_args()
@@ -57,26 +59,66 @@ def parse():
     return a
 
 
-def cpu_baseline(ds, ncols, nproma=32):
-    """Reference C kernel (oracle/_ref, compiled from the reference sources) when
-    present, else the oracle restatement; OpenMP over NPROMA blocks on the host
-    cores (cloudsc_driver.c:183-217).  Returns the cpu_baseline object."""
+def cpu_baseline(ca, ds, nthreads):
+    """BASELINE.md §4 on this box's host cores, rank 0 at N=1 only: the reference
+    C kernel (oracle/_ref, compiled from src/cloudsc_c/cloudsc/cloudsc_c.c) in
+    the C dwarf's OpenMP block loop, timed around the loop only
+    (cloudsc_driver.c:181-231), at `1 16384 32` (config 1) and `T 163840 {16,32}`
+    (T = the host threads of this box's share), each run validated against
+    reference.h5 with the ERROR_PRINT statistics.  value = the faster of the two
+    163840-column runs.  The library's own CPU variant (cloudsc_cpu_run) is timed
+    beside it on the same states ("cpu_variant")."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
     import oracle
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     kind = "reference" if oracle.ref_available() else "port"
-    best = None
-    for _ in range(2):
+    eps10 = 10 * np.finfo(np.float64).eps
+    runs, product = [], []
+    for nth, ncols, nproma in ((1, 16384, 32), (nthreads, 163840, 16), (nthreads, 163840, 32)):
+        st = ca.make_host_state(ds, ncols, nproma, ca.FP64)
+        plude0 = st.arrays["plude"].copy()
         if kind == "reference":
-            _, secs = oracle.run_ref(ds, ncols, nproma, nthreads=nthreads)
+            secs = oracle.run_ref_state(ds, st, nthreads=nth)
         else:
-            _, secs = oracle.run_oracle(ds, ncols, nproma, nthreads=nthreads)
-        best = secs if best is None else min(best, secs)
-    return {"value": ncols / best, "unit": "columns/s", "cores": nthreads, "kind": kind,
-            "sample": "%d columns of the same fp64 workload (g %% 100 expansion, KLEV=137), NPROMA=%d, "
-                      "%d OpenMP threads, best of 2 block loops (%s)" % (
-                          ncols, nproma, nthreads,
-                          "src/cloudsc_c/cloudsc/cloudsc_c.c" if kind == "reference" else "oracle/cloudsc_oracle.c")}
+            _, secs = oracle.run_oracle(ds, ncols, nproma, nthreads=nth)
+        worst = ca.validate_host_state(ds, st) if kind == "reference" else None
+        runs.append({"cmd": "%d %d %d" % (nth, ncols, nproma), "columns_per_s": round(ncols / secs, 1),
+                     "ms": round(1e3 * secs, 2), "worst_rel_l1": worst,
+                     "validated": bool(worst is not None and worst <= eps10)})
+        np.copyto(st.arrays["plude"], plude0)
+        secs = ca.cpu_run_state(ds, st, nthreads=nth)
+        w = ca.validate_host_state(ds, st)
+        product.append({"cmd": "%d %d %d" % (nth, ncols, nproma), "columns_per_s": round(ncols / secs, 1),
+                        "ms": round(1e3 * secs, 2), "worst_rel_l1": w, "validated": bool(w <= eps10)})
+        del st, plude0
+    full = [r for r in runs if r["cmd"].split()[1] == "163840"]
+    best = max(full, key=lambda r: r["columns_per_s"])
+    return {"value": best["columns_per_s"], "unit": "columns/s", "cores": nthreads, "kind": kind,
+            "sample": "%s `%s` (163840 columns, the full workload; the faster NPROMA of 16/32), OpenMP block "
+                      "loop timed like cloudsc_driver.c:181-231, validated vs reference.h5" % (
+                          "reference kernel src/cloudsc_c/cloudsc/cloudsc_c.c compiled from its sources"
+                          if kind == "reference" else "oracle restatement", best["cmd"]),
+            "runs": runs,
+            "cpu_variant": {"what": "this library's cloudsc_cpu_run (the GPU kernels' phase functions "
+                                    "compiled for the host), same states", "runs": product}}
+
+
+def roofline_traffic(ca, path, key):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC passes, only if they
+    were measured on the current kernel sources (kernel_source_hash)."""
+    if not os.path.exists(path):
+        return None, "no PMC measurement (%s)" % os.path.relpath(path, REPO)
+    try:
+        entry = json.load(open(path)).get(key)
+    except Exception as e:            # an unreadable file is reported, not fatal
+        return None, "unreadable %s: %s" % (path, e)
+    if not entry:
+        return None, "no PMC measurement for %s" % key
+    if entry.get("kernel_source_hash") != ca.kernel_source_hash():
+        return None, "PMC measurement is stale (measured on kernel sources %s, current %s)" % (
+            entry.get("kernel_source_hash"), ca.kernel_source_hash())
+    return entry["hbm_bytes_per_launch"], "rocprofv3 2xFETCH_SIZE+WRITE_SIZE per launch, kernel sources %s" % (
+        entry["kernel_source_hash"])
 
 
 def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=32, nstreams=4):
@@ -144,15 +186,11 @@ def main():
     value = total_cols * args.steps / wall
     bpc = BYTES_PER_COL[prec]
     achieved = bpc * args.ngptot / (k_avg_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            key = "%s_%s_%d_%d" % (args.variant, args.precision, args.ngptot, args.nproma)
-            if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
+    traffic, traffic_src = roofline_traffic(
+        ca, args.traffic_json, "%s_%s_%d_%d" % (args.variant, args.precision, args.ngptot, args.nproma))
+    peak_meas = None
+    if not args.no_hbm_peak:
+        peak_meas = ca.hbm_copy_gbps(device, 4 << 30, 10)
     line = {
         "metric": "grid-columns/sec at NGPTOT=163840 KLEV=137 fp64; achieved HBM GB/s vs peak",
         "value": round(value, 1),
@@ -165,7 +203,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64" if prec == ca.FP64 else "f32",
-        "data": "reference 100-column IFS state (tests/golden/cloudsc100, from the reference's data/) "
+        "data": "reference 100-column IFS state (data/cloudsc100, from the reference's data/) "
                 "expanded on the device with g % 100",
         "config": {"workload": "CLOUDSC %s, NGPTOT=%d per GPU, KLEV=%d, NPROMA=%d, %s" % (
             {ca.VARIANT_KSEG: "SCC-k-caching (persistent, level-segmented)",
@@ -178,12 +216,21 @@ def main():
         "validation_worst_rel_l1": worst,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_column": bpc},
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_column": bpc,
+                     "algorithmic_bytes_per_launch": bpc * args.ngptot},
     }
+    if peak_meas:
+        line["roofline"]["achievable_peak"] = {
+            "value": round(peak_meas, 1), "unit": "GB/s",
+            "method": "STREAM copy on this device in this run (cloudsc_hbm_copy_gbps: 2 x 4 GiB, 16 B/lane "
+                      "non-temporal, best of 10)"}
+        line["roofline"]["frac_of_achievable"] = round(achieved / peak_meas, 4)
     if args.transfer and world == 1:
         line["pcie_inclusive"] = transfer_rate(ca, ds, args, prec, variant)
     if not args.no_cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(ds, min(args.cpu_sample, args.ngptot))
+        nth = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(ca, ds, nth)
     print(json.dumps(line), flush=True)
     ctl.close()
 

@@ -31,7 +31,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libcloudsc_amd.so")
-GOLDEN_DIR = os.path.join(REPO, "tests", "golden", "cloudsc100")
+DATA_DIR = os.path.join(REPO, "data", "cloudsc100")   # the reference's data/ arrays (tools/make_fixtures.py)
 
 NCLV = 5
 FP64, FP32 = 8, 4
@@ -187,7 +187,7 @@ class Dataset:
                        {k: v.copy() for k, v in self.reference.items()})
 
 
-def load_dataset(path: str = GOLDEN_DIR, with_reference: bool = True) -> Dataset:
+def load_dataset(path: str = DATA_DIR, with_reference: bool = True) -> Dataset:
     """Read a raw dataset directory (``input_<NAME>.dat``, ``reference_<NAME>.dat``,
     ``params.txt``, ``manifest.json``) as written by tools/make_fixtures.py."""
     man = json.load(open(os.path.join(path, "manifest.json")))
@@ -257,15 +257,44 @@ class HostState:
         return f
 
 
+_KIND_CODE = {"2d": 0, "2dh": 1, "3d": 2, "1d": 3}
+_io = None
+
+
+def io_lib():
+    """libcloudsc_io.so (host-only dataset plumbing of the C driver), or None if
+    it is not built -- then the numpy forms below are used (same results)."""
+    global _io
+    if _io is None:
+        path = os.path.join(HERE, "libcloudsc_io.so")
+        if not os.path.exists(path):
+            return None
+        lib = C.CDLL(path)
+        lib.cloudsc_io_expand.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.c_longlong, C.c_int, C.c_void_p]
+        lib.cloudsc_io_field_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                               C.c_int, C.c_int, C.c_longlong, C.c_void_p]
+        _io = lib
+    return _io
+
+
 def make_host_state(ds: Dataset, ngptot: int, nproma: int, precision: int = FP64,
                     col_offset: int = 0) -> HostState:
     real = np.float64 if precision == FP64 else np.float32
     nb = nblocks_of(ngptot, nproma)
     arrays = {}
+    io = io_lib()
     for name, arr in ds.inputs.items():
         kind = ALL_FIELDS[name]
-        arrays[name] = expand(arr, kind, ngptot, nproma, col_offset,
-                              dtype=np.int32 if name == "ktype" else real)
+        dt = np.int32 if name == "ktype" else real
+        if io is not None and arr.dtype == (np.int32 if name == "ktype" else np.float64):
+            src = np.ascontiguousarray(arr)
+            out = np.empty((nb,) + field_shape(kind, ds.klev, nproma), dtype=dt)
+            io.cloudsc_io_expand(src.ctypes.data, _KIND_CODE[kind], int(name == "ktype"), ds.klev, ds.klon,
+                                 ngptot, nproma, col_offset, out.itemsize, out.ctypes.data)
+            arrays[name] = out
+        else:
+            arrays[name] = expand(arr, kind, ngptot, nproma, col_offset, dtype=dt)
     for name, kind in OUTPUT_FIELDS.items():
         shp = (nb,) + field_shape(kind, ds.klev, nproma)
         arrays[name] = np.full(shp, np.nan, dtype=real)                # callee must write all
@@ -308,7 +337,9 @@ def state_outputs_to_template(arrays: Dict[str, np.ndarray], ngptot: int) -> Dic
 # GPU library (no fallback)
 # ---------------------------------------------------------------------------
 class CloudscError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 _lib = None
@@ -345,8 +376,92 @@ def gpu_lib(path: Optional[str] = None):
                                                  C.c_int, C.c_int, C.c_int, C.POINTER(Fields)]
     lib.cloudsc_host_pipeline_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
     lib.cloudsc_host_pipeline_destroy.argtypes = [C.c_void_p]
+    lib.cloudsc_gpu_check.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+    lib.cloudsc_hbm_copy_gbps.argtypes = [C.c_int, C.c_longlong, C.c_int, C.POINTER(C.c_double)]
+    lib.cloudsc_cpu_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Params), C.POINTER(Fields),
+                                    C.POINTER(C.c_double)]
+    lib.cloudsc_debug_set_kseg_spin_limit.argtypes = [C.c_longlong]
+    lib.cloudsc_debug_set_kseg_schedule.argtypes = [C.c_int, C.c_int]
     _lib = lib
     return lib
+
+
+EHANDOFF = -7
+
+
+def kseg_schedule(nseg: int = 0, grid: int = 0) -> None:
+    """Diagnostic override of the KSEG schedule (0 = default); results do not change."""
+    check(gpu_lib().cloudsc_debug_set_kseg_schedule(nseg, grid))
+
+
+def kseg_spin_limit(limit: int = -1) -> None:
+    """Diagnostic: polls before a KSEG consumer gives up (negative = default, 0 = fail at once)."""
+    check(gpu_lib().cloudsc_debug_set_kseg_spin_limit(limit))
+
+
+def cpu_run(ds: "Dataset", ngptot: int, nproma: int = 32, nthreads: int = 0, col_offset: int = 0):
+    """The library's CPU variant (cloudsc_cpu_run, BASELINE.json config 1) on a
+    host block-layout state expanded from ds.  Returns (HostState, seconds).
+    Explicitly a CPU run -- it is never used in place of a GPU run."""
+    st = make_host_state(ds, ngptot, nproma, FP64, col_offset)
+    return st, cpu_run_state(ds, st, nthreads)
+
+
+def cpu_run_state(ds: "Dataset", st: "HostState", nthreads: int = 0) -> float:
+    """cloudsc_cpu_run on an already expanded host state (plude is INOUT: the
+    caller restores it between runs).  Returns seconds of the block loop."""
+    p = Params.from_dict(ds.params)
+    f = st.fields()
+    secs = C.c_double()
+    check(gpu_lib().cloudsc_cpu_run(nthreads, st.ngptot, st.nproma, st.klev, C.byref(p), C.byref(f),
+                                    C.byref(secs)))
+    return secs.value
+
+
+def validate_host_state(ds: "Dataset", st: "HostState") -> float:
+    """Worst per-field relative L1 error (ERROR_PRINT, validate_mod.F90:263-296)
+    of a host state's 21 outputs against ds.reference replicated with g % klon."""
+    worst = 0.0
+    io = io_lib()
+    cols = None
+    for _, k in VALIDATED:
+        if io is not None:
+            ref = np.ascontiguousarray(ds.reference[k], dtype=np.float64)
+            fld = np.ascontiguousarray(st.arrays[k])
+            stt = Stats()
+            io.cloudsc_io_field_stats(ref.ctypes.data, _KIND_CODE[ALL_FIELDS[k]], ds.klev, ds.klon, fld.ctypes.data,
+                                      fld.itemsize, st.ngptot, st.nproma, 0, C.byref(stt))
+            errsum, refsum = stt.errsum, stt.refsum
+        else:
+            cols = np.arange(st.ngptot) % ds.klon if cols is None else cols
+            out = blocks_to_columns(st.arrays[k], st.ngptot)
+            _, _, _, errsum, refsum = field_stats(out, np.take(ds.reference[k], cols, axis=-1))
+        worst = max(worst, rel_error(errsum, refsum)[0])
+    return worst
+
+
+def kernel_source_hash() -> str:
+    """SHA-256 (16 hex digits) of the kernel sources and the library's build
+    flags: the key that ties a measured PMC traffic figure to the kernel it was
+    measured on (bench.py drops a figure whose hash is not the current one)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(HERE, "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".hip", ".h")):
+            h.update(name.encode())
+            with open(os.path.join(csrc, name), "rb") as fh:
+                h.update(fh.read())
+    with open(os.path.join(HERE, "Makefile"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def hbm_copy_gbps(device: int = 0, nbytes: int = 4 << 30, reps: int = 10) -> float:
+    """Achievable HBM bandwidth of the device (STREAM copy, GB/s)."""
+    g = C.c_double()
+    check(gpu_lib().cloudsc_hbm_copy_gbps(device, nbytes, reps, C.byref(g)))
+    return g.value
 
 
 def device_count() -> int:
@@ -360,7 +475,7 @@ def check(rc: int) -> None:
     if rc != 0:
         lib = gpu_lib()
         raise CloudscError("cloudsc error %d: %s (hip: %s)" % (
-            rc, lib.cloudsc_strerror(rc).decode(), (lib.cloudsc_last_hip_error() or b"").decode()))
+            rc, lib.cloudsc_strerror(rc).decode(), (lib.cloudsc_last_hip_error() or b"").decode()), rc)
 
 
 def make_template(ds: Dataset, keep: list) -> Template:

@@ -3,18 +3,30 @@
 //
 // The YOMCST / YOETHF constants and the TECLDP tuning parameters the kernel
 // reads (reference: src/cloudsc_c/cloudsc/{yomcst_c,yoethf_c,yoecldp_c}.h) live
-// in __constant__ memory, one mirror per precision; uniform across the grid,
-// so every access is a scalar (s_load) read.  A few derived constants that the
+// in a device-memory block per parameter set, one mirror per precision, passed
+// to every launch by pointer and read through the constant address space:
+// uniform across the grid, so every access is a scalar (s_load) read.  A few derived constants that the
 // reference recomputes per point (1/PTSPHY, RD/RCPD, 1/(PTSPHY*RG), ...) are
 // folded on the host with the SAME IEEE operation, so results do not change.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <type_traits>
 
 #include "cloudsc_libm.h"
 
 namespace cloudsc {
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// host pass: the float overloads of the C math functions the phase functions
+// call (in the device pass the HIP device library's overloads are used)
+using std::copysign;
+using std::fabs;
+using std::fmax;
+using std::fmin;
+using std::sqrt;
+#endif
 
 template <typename real>
 struct DevParams {
@@ -47,6 +59,14 @@ struct DevParams {
   int nssopt, ncldtop, laericesed, laericeauto;
 };
 
+// The phase functions of the physics (cloudsc_kcache.h) and the helpers below
+// compile for the device (the kernels) and for the host (cloudsc_cpu_run,
+// cloudsc_cpu.hip: the same source as the explicitly selected CPU variant).
+// The few helpers whose device form is target-specific (register laundering,
+// the reciprocal-based division, the LDS-table exp/pow) have a plain host form
+// selected on __HIP_DEVICE_COMPILE__; both forms round identically.
+#define CLOUDSC_HD __host__ __device__ __forceinline__
+
 // Address-space-4 (constant) pointer: loads through it are scalar (s_load).
 #define CLOUDSC_AS4 __attribute__((address_space(4)))
 template <typename T>
@@ -61,9 +81,7 @@ using cptr = const CLOUDSC_AS4 T*;
 // cache hit -- at no register cost.
 template <typename T>
 __device__ __forceinline__ cptr<T> launder_uniform(cptr<T> p) {
-#ifndef CLOUDSC_NO_LAUNDER
   asm volatile("" : "+s"(p));
-#endif
   return p;
 }
 // A parameter value materialised as a value (scalar register) at this point.
@@ -71,13 +89,17 @@ __device__ __forceinline__ cptr<T> launder_uniform(cptr<T> p) {
 // into ONE load through a selected address -- a per-lane (vector, or flat via
 // a stack slot) load with a full memory wait inside the level loop.
 template <typename T>
-__device__ __forceinline__ T sval(T v) {
+CLOUDSC_HD T sval(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("" : "+s"(v));
+#endif
   return v;
 }
 template <typename T>
-__device__ __forceinline__ T launder_vgpr(T v) {
+CLOUDSC_HD T launder_vgpr(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("" : "+v"(v));
+#endif
   return v;
 }
 
@@ -85,9 +107,7 @@ __device__ __forceinline__ T launder_vgpr(T v) {
 // (the JPRB=sp semantics, parkind1.F90:40-43).
 #define R(x) (real)(x)
 
-// Device math used by the kernels.  One place to swap implementations; the
-// CLOUDSC_ABLATE_* macros exist only for timing-only diagnostic builds (they
-// give wrong results) that price each function's share of the kernel.
+// Device math used by the kernels.
 //
 // fp64 exp/pow: the reference CPU build's own algorithms (cloudsc_libm.h),
 // so that the GPU rounds every exp/pow exactly as the reference kernel does.
@@ -97,8 +117,6 @@ __device__ __forceinline__ T launder_vgpr(T v) {
 // read from global memory instead would be counted by vmcnt, and waiting for
 // it inside a physics branch would drain the software-pipelined level loads
 // (vmcnt(0)); LDS reads are counted by lgkmcnt.
-// CLOUDSC_OCML_EXP_POW selects OCML's exp/powr instead (about 1 ulp, not the
-// reference's rounding).
 __constant__ __attribute__((aligned(16))) unsigned long long g_cl_exp_tab[2 * 128] = {CLOUDSC_LIBM_EXP_TAB};
 __constant__ __attribute__((aligned(16))) double g_cl_log_tab[4 * 128] = {CLOUDSC_LIBM_LOG_TAB};
 typedef unsigned long long cl_u64x2 __attribute__((ext_vector_type(2)));
@@ -148,11 +166,9 @@ struct ConstLibmTabs {
     return {a.x, a.y, g_cl_log_tab[4 * i + 2]};
   }
 };
-#ifdef CLOUDSC_LIBM_COLD_INLINE   // experiment: cold paths inlined at every call site
-#define CLOUDSC_LIBM_COLD_ATTR __forceinline__
-#else
+// (inlining them at every call site measured +35 % kernel time: code size and
+// register pressure)
 #define CLOUDSC_LIBM_COLD_ATTR __noinline__ __attribute__((pure))
-#endif
 __device__ CLOUDSC_LIBM_COLD_ATTR double cl_exp_cold(double x) { return cloudsc_libm::exp(x, ConstLibmTabs{}); }
 __device__ CLOUDSC_LIBM_COLD_ATTR double cl_pow_cold(double x, double y) { return cloudsc_libm::pow(x, y, ConstLibmTabs{}); }
 __device__ CLOUDSC_LIBM_COLD_ATTR float cl_expf_cold(float x) { return cloudsc_libm::expf(x, ConstLibmTabsF{}); }
@@ -169,7 +185,6 @@ struct DevLibmCold {
 // a barrier).
 template <typename real>
 __device__ __forceinline__ void libm_tables_to_lds() {
-#ifndef CLOUDSC_OCML_EXP_POW
   if constexpr (std::is_same<real, double>::value) {
     for (int i = threadIdx.x; i < 128; i += blockDim.x) {
       s_cl_exp_tab[i] = ((const cl_u64x2*)g_cl_exp_tab)[i];
@@ -184,69 +199,49 @@ __device__ __forceinline__ void libm_tables_to_lds() {
     }
     __syncthreads();
   }
-#endif
 }
 
-#ifdef CLOUDSC_NOINLINE_POW
-__device__ __attribute__((noinline)) double cl_pow_ool(double x, double y);
-__device__ __attribute__((noinline)) float cl_pow_ool(float x, float y);
-#endif
 // pow is only ever applied to non-negative bases here (densities, ratios of
-// positive quantities, temperatures, slope parameters), where OCML's powr (the
-// x >= 0 power: no negative-base / integer-exponent handling) is the same
-// core computation as pow without the special-case fix-ups.
-extern "C" __device__ double __ocml_powr_f64(double, double);
-extern "C" __device__ float __ocml_powr_f32(float, float);
-#ifdef CLOUDSC_OCML_EXP_POW
-#define CLOUDSC_OCML_EXP
-#define CLOUDSC_OCML_POW
-#endif
+// positive quantities, temperatures, slope parameters): the hot path of
+// cloudsc_libm::pow_split handles exactly those, everything else goes to the
+// complete out-of-line function.
 __device__ __forceinline__ double cl_powr(double x, double y) {
-#ifdef CLOUDSC_OCML_POW
-  return __ocml_powr_f64(x, y);
-#else
   return cloudsc_libm::pow_split(x, y, LdsLibmTabs{}, DevLibmCold{});
-#endif
 }
 __device__ __forceinline__ float cl_powr(float x, float y) {
-#ifdef CLOUDSC_OCML_POW
-  return __ocml_powr_f32(x, y);
-#else
   return cloudsc_libm::powf_split(x, y, LdsLibmTabsF{}, DevLibmCold{});
-#endif
 }
-__device__ __forceinline__ double cl_exp_impl(double x) {
-#ifdef CLOUDSC_OCML_EXP
-  return exp(x);
-#else
-  return cloudsc_libm::exp_split(x, LdsLibmTabs{}, DevLibmCold{});
-#endif
+__device__ __forceinline__ double cl_exp_impl(double x) { return cloudsc_libm::exp_split(x, LdsLibmTabs{}, DevLibmCold{}); }
+__device__ __forceinline__ float cl_exp_impl(float x) { return cloudsc_libm::expf_split(x, LdsLibmTabsF{}, DevLibmCold{}); }
+// host forms: the same algorithms with the tables read from host memory
+struct HostLibmCold {
+  double exp(double x) const { return cloudsc_libm::exp(x, cloudsc_libm::HostTabs{}); }
+  double pow(double x, double y) const { return cloudsc_libm::pow(x, y, cloudsc_libm::HostTabs{}); }
+  float expf(float x) const { return cloudsc_libm::expf(x, cloudsc_libm::HostTabsF{}); }
+  float powf(float x, float y) const { return cloudsc_libm::powf(x, y, cloudsc_libm::HostTabsF{}); }
+};
+inline double cl_powr_host(double x, double y) {
+  return cloudsc_libm::pow_split(x, y, cloudsc_libm::HostTabs{}, HostLibmCold{});
 }
-__device__ __forceinline__ float cl_exp_impl(float x) {
-#ifdef CLOUDSC_OCML_EXP
-  return expf(x);
-#else
-  return cloudsc_libm::expf_split(x, LdsLibmTabsF{}, DevLibmCold{});
-#endif
+inline float cl_powr_host(float x, float y) {
+  return cloudsc_libm::powf_split(x, y, cloudsc_libm::HostTabsF{}, HostLibmCold{});
 }
+inline double cl_exp_host(double x) { return cloudsc_libm::exp_split(x, cloudsc_libm::HostTabs{}, HostLibmCold{}); }
+inline float cl_exp_host(float x) { return cloudsc_libm::expf_split(x, cloudsc_libm::HostTabsF{}, HostLibmCold{}); }
 template <typename real>
-__device__ __forceinline__ real cl_pow(real x, real y) {
-#if defined(CLOUDSC_ABLATE_POW)
-  return x * y;
-#elif defined(CLOUDSC_NOINLINE_POW)
-  return cl_pow_ool(x, y);
-#elif defined(CLOUDSC_LIBM_POW)
-  return pow(x, y);
-#else
+CLOUDSC_HD real cl_pow(real x, real y) {
+#if defined(__HIP_DEVICE_COMPILE__)
   return cl_powr(x, y);
+#else
+  return cl_powr_host(x, y);
 #endif
 }
 template <typename real>
-__device__ __forceinline__ real cl_exp(real x) {
-#ifdef CLOUDSC_ABLATE_EXP
-  return x + (real)1.0;
-#else
+CLOUDSC_HD real cl_exp(real x) {
+#if defined(__HIP_DEVICE_COMPILE__)
   return cl_exp_impl(x);
+#else
+  return cl_exp_host(x);
 #endif
 }
 
@@ -265,10 +260,9 @@ __device__ __forceinline__ real cl_exp(real x) {
 // ratios of physical quantities), and the A/B identity check
 // (tools/ab_compare.py: reference state, scenarios, random perturbations,
 // NSSOPT, aerosol flags, fp32, 163840 columns) confirms identical output bits.
-// CLOUDSC_IEEE_DIV restores the plain operator.
-__device__ __forceinline__ double cl_div(double n, double d) {
-#ifdef CLOUDSC_IEEE_DIV
-  return n / d;
+CLOUDSC_HD double cl_div(double n, double d) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return n / d;       // host: the IEEE division itself
 #else
   double r = __builtin_amdgcn_rcp(d);
   double e = __builtin_fma(-d, r, 1.0);
@@ -280,8 +274,8 @@ __device__ __forceinline__ double cl_div(double n, double d) {
   return __builtin_fma(rem, r, q);
 #endif
 }
-__device__ __forceinline__ float cl_div(float n, float d) {
-#ifdef CLOUDSC_IEEE_DIV
+CLOUDSC_HD float cl_div(float n, float d) {
+#if !defined(__HIP_DEVICE_COMPILE__)
   return n / d;
 #else
   float r = __builtin_amdgcn_rcpf(d);
@@ -296,24 +290,24 @@ __device__ __forceinline__ float cl_div(float n, float d) {
 }
 // explicit-precision form, cl_div<real>(a, b)
 template <typename real>
-__device__ __forceinline__ real cl_div(typename std::common_type<real>::type n, typename std::common_type<real>::type d) {
+CLOUDSC_HD real cl_div(typename std::common_type<real>::type n, typename std::common_type<real>::type d) {
   return cl_div(static_cast<real>(n), static_cast<real>(d));
 }
 
 // FOEALFA (src/common/include/fcttre.func.h; inlined at cloudsc_c.c:588,831,1162-1174)
 template <typename real, typename P>
-__device__ __forceinline__ real foealfa(const P& c, real t) {
+CLOUDSC_HD real foealfa(const P& c, real t) {
   real x = (fmax(c.rtice, fmin(c.rtwat, t)) - c.rtice) * c.rtwat_rtice_r;
   return fmin(R(1.0), x * x);            // pow(x,2) == x*x (both rounded once)
 }
 template <typename real, typename P>
-__device__ __forceinline__ real exp_liq(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3les * (t - c.rtt), t - c.r4les)); }
+CLOUDSC_HD real exp_liq(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3les * (t - c.rtt), t - c.r4les)); }
 template <typename real, typename P>
-__device__ __forceinline__ real exp_ice(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3ies * (t - c.rtt), t - c.r4ies)); }
+CLOUDSC_HD real exp_ice(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3ies * (t - c.rtt), t - c.r4ies)); }
 
 // alfa*R5ALVCP/(T-R4LES)^2 + (1-alfa)*R5ALSCP/(T-R4IES)^2 (cloudsc_c.c:1166,1220)
 template <typename real, typename P>
-__device__ __forceinline__ real foedem_term(const P& c, real t, real alfa) {
+CLOUDSC_HD real foedem_term(const P& c, real t, real alfa) {
   real dl = t - c.r4les, di = t - c.r4ies;
   return ((alfa * c.r5alvcp) * cl_div<real>(R(1.0), dl * dl)) + (((R(1.0) - alfa) * c.r5alscp) * cl_div<real>(R(1.0), di * di));
 }

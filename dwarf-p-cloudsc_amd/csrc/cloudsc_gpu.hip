@@ -1,44 +1,42 @@
 // cloudsc_gpu.hip -- libcloudsc_amd.so: the C ABI of include/cloudsc_amd.h on
 // top of the hand-written CDNA4 kernels.
 //
-//   * parameters -> __constant__ mirrors (fp64 + fp32), one copy per device
-//     (replaces the TECLDP device struct + 28 by-value scalars of
-//     src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:383,412-416)
+//   * parameters -> a device-memory block per parameter set (fp64 + fp32
+//     mirrors, host-folded), passed to every launch by pointer and read with
+//     scalar loads through the constant address space.  Each device has a
+//     default set (cloudsc_gpu_init); every state and host pipeline owns its
+//     own, so two states with different parameters never see each other's.
+//     This replaces the TECLDP device struct passed by pointer + the 28
+//     by-value scalars of src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:312,383,411-416.
 //   * cloudsc_gpu_run: one launch, NPROMA block -> workgroup, column -> lane
-//   * cloudsc_state_*: device-side expansion from the KLON-column template
-//     (g % klon of the GLOBAL column, so shards are bit-identical to an
-//     unsharded run), per-step timing with HIP events on the state's stream,
-//     and device-side validation statistics against the KLON-column reference.
+//     (KCACHE, SCC) or a persistent work queue of (level segment, 64-column
+//     sub-block) items (KSEG).
 //
-// No CPU fallback: every entry point fails with a CLOUDSC_E* code if HIP or
-// the device is unavailable.
+// No CPU fallback: every GPU entry point fails with a CLOUDSC_E* code if HIP or
+// the device is unavailable.  (cloudsc_cpu_run, cloudsc_cpu.cpp, is a separate,
+// explicitly selected host variant, never substituted for a GPU run.)
 #include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "cloudsc_amd.h"
 #include "cloudsc_dev.h"
 #include "cloudsc_internal.h"
 #include "cloudsc_kcache.h"
+#include "cloudsc_params.h"
 #include "cloudsc_scc.h"
 
 using namespace cloudsc;
 using namespace cloudsc_impl;
 
 // ---------------------------------------------------------------------------
-// __constant__ parameter mirrors
+// error text (per calling thread)
 // ---------------------------------------------------------------------------
-#ifdef CLOUDSC_NOINLINE_POW
-__device__ __attribute__((noinline)) double cloudsc::cl_pow_ool(double x, double y) { return pow(x, y); }
-__device__ __attribute__((noinline)) float cloudsc::cl_pow_ool(float x, float y) { return pow(x, y); }
-#endif
-__constant__ DevParams<double> g_params_dp;
-__constant__ DevParams<float> g_params_sp;
-
 namespace cloudsc_impl {
 thread_local char g_hip_err[256] = "";
 int hip_fail(hipError_t e, const char* what) {
@@ -48,51 +46,22 @@ int hip_fail(hipError_t e, const char* what) {
 void set_error_text(const char* text) { snprintf(g_hip_err, sizeof(g_hip_err), "%s", text); }
 }  // namespace cloudsc_impl
 
+// ---------------------------------------------------------------------------
+// parameter sets
+// ---------------------------------------------------------------------------
 namespace {
 
-bool g_inited[kMaxDevices] = {false};
-bool g_aer[kMaxDevices] = {false};      // LAERICESED || LAERICEAUTO of the device's parameters
-int g_ncldtop[kMaxDevices] = {0};       // NCLDTOP of the device's parameters (KSEG segment bounds)
+// device layout of one parameter set: the fp64 mirror, then the fp32 one
+constexpr size_t kSpOffset = (sizeof(DevParams<double>) + 255) & ~(size_t)255;
+constexpr size_t kParamBlockBytes = kSpOffset + sizeof(DevParams<float>);
 
-template <typename real>
-DevParams<real> fold_params(const cloudsc_params_t& p) {
-  DevParams<real> d;
-  std::memset(&d, 0, sizeof(d));
-#define CP(n) d.n = (real)p.n
-  CP(ptsphy); CP(rg); CP(rd); CP(retv); CP(rlvtt); CP(rlstt); CP(rtt); CP(rv);
-  CP(r2es); CP(r3les); CP(r3ies); CP(r4les); CP(r4ies); CP(r5les); CP(r5ies); CP(r5alvcp); CP(r5alscp);
-  CP(ralvdcp); CP(ralsdcp); CP(ralfdcp); CP(rtwat); CP(rtice); CP(rtwat_rtice_r); CP(rkoop1); CP(rkoop2);
-  CP(ramid); CP(rprecrhmax); CP(rtaumel); CP(ramin); CP(rlmin); CP(rlcritsnow); CP(rsnowlin2);
-  CP(riceinit); CP(rvice); CP(rvrain); CP(rvsnow); CP(rthomo); CP(rcovpmin); CP(rnice); CP(rcldtopcf);
-  CP(rdepliqrefrate); CP(rdepliqrefdepth); CP(rvrfactor); CP(rclcrit_sea); CP(rclcrit_land);
-  CP(rcl_kkaac); CP(rcl_kkbac); CP(rcl_kkaau); CP(rcl_kkbauq); CP(rcl_kkbaun); CP(rcl_kk_cloud_num_sea);
-  CP(rcl_kk_cloud_num_land); CP(rcl_const1s); CP(rcl_const7s); CP(rcl_const8s); CP(rdensref);
-  CP(rcl_cdenom1); CP(rcl_cdenom2); CP(rcl_cdenom3); CP(rcl_const1r); CP(rcl_const2r); CP(rcl_const3r);
-  CP(rcl_const4r); CP(rcl_fac1); CP(rcl_fac2); CP(rcl_const5r); CP(rcl_const6r); CP(rcl_fzrab);
-#undef CP
-  // Host folding in the working precision: the same single IEEE operation the
-  // reference evaluates per point (x86-64 host float/double arithmetic is IEEE).
-  const real ptsphy = (real)p.ptsphy, rg = (real)p.rg, rd = (real)p.rd, rcpd = (real)p.rcpd;
-  volatile real one = (real)1.0;   // keep the compiler from re-associating
-  d.zqtmst = one / ptsphy;
-  d.zrdcp = rd / rcpd;
-  d.zrg_r = one / rg;
-  d.zrldcp = one / ((real)p.ralsdcp - (real)p.ralvdcp);
-  d.zinv_tsrg = one / (ptsphy * rg);
-  d.half_rg = (real)0.5 * rg;
-  d.zldifdt0 = (real)p.rcldiff * ptsphy;
-  d.zldifdt_conv = (real)p.rcldiff_convi * d.zldifdt0;
-  d.zfaci_koop = ptsphy / (real)p.rkooptau;
-  d.zzco_snow = ptsphy * (real)p.rsnowlin1;
-  d.rv_rd = (real)p.rv / rd;
-  d.rg_rpecons = rg * (real)p.rpecons;
-  d.one_m_ramin = one - (real)p.ramin;
-  d.nssopt = p.nssopt;
-  d.ncldtop = p.ncldtop;
-  d.laericesed = p.laericesed;
-  d.laericeauto = p.laericeauto;
-  return d;
-}
+// the per-device default parameter sets (cloudsc_gpu_init)
+std::mutex g_default_mu;
+ParamSet g_default[kMaxDevices];
+
+}  // namespace
+
+namespace cloudsc_impl {
 
 int check_params(const cloudsc_params_t* p) {
   if (!p) return CLOUDSC_EINVAL;
@@ -102,8 +71,73 @@ int check_params(const cloudsc_params_t* p) {
   return CLOUDSC_OK;
 }
 
+int param_set_upload(ParamSet* ps, int device, const cloudsc_params_t* p) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(device));
+  if (!ps->dev) {
+    hipError_t e = hipMalloc(&ps->dev, kParamBlockBytes);
+    if (e != hipSuccess) { ps->dev = nullptr; hip_fail(e, "hipMalloc(params)"); return CLOUDSC_ENOMEM; }
+  }
+  std::vector<char> blk(kParamBlockBytes, 0);
+  const DevParams<double> dp = fold_params<double>(*p);
+  const DevParams<float> sp = fold_params<float>(*p);
+  std::memcpy(blk.data(), &dp, sizeof(dp));
+  std::memcpy(blk.data() + kSpOffset, &sp, sizeof(sp));
+  HIPCHK(hipMemcpy(ps->dev, blk.data(), kParamBlockBytes, hipMemcpyHostToDevice));
+  ps->device = device;
+  ps->aer = p->laericesed || p->laericeauto;
+  ps->ncldtop = p->ncldtop;
+  return CLOUDSC_OK;
+}
+
+int param_set_copy(ParamSet* dst, const ParamSet* src) {
+  if (!src || !src->dev) return CLOUDSC_ENOINIT;
+  HIPCHK(hipSetDevice(src->device));
+  if (!dst->dev) {
+    hipError_t e = hipMalloc(&dst->dev, kParamBlockBytes);
+    if (e != hipSuccess) { dst->dev = nullptr; hip_fail(e, "hipMalloc(params)"); return CLOUDSC_ENOMEM; }
+  }
+  HIPCHK(hipMemcpy(dst->dev, src->dev, kParamBlockBytes, hipMemcpyDeviceToDevice));
+  dst->device = src->device;
+  dst->aer = src->aer;
+  dst->ncldtop = src->ncldtop;
+  return CLOUDSC_OK;
+}
+
+void param_set_free(ParamSet* ps) {
+  if (ps && ps->dev) {
+    (void)hipSetDevice(ps->device);
+    (void)hipFree(ps->dev);
+    ps->dev = nullptr;
+  }
+}
+
+const ParamSet* device_default_params(int device) {
+  if (device < 0 || device >= kMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  return g_default[device].dev ? &g_default[device] : nullptr;
+}
+
+bool fields_complete(const cloudsc_fields_t* f) {
+  const void* req[] = {f->pt, f->pq, f->tendency_tmp_t, f->tendency_tmp_q, f->tendency_tmp_a,
+                       f->tendency_tmp_cld, f->pvfl, f->pvfi, f->phrsw, f->phrlw, f->pvervel, f->pap,
+                       f->paph, f->plsm, f->ktype, f->plu, f->psnde, f->pmfu, f->pmfd, f->pa, f->pclv,
+                       f->psupsat, f->plude, f->tendency_loc_t, f->tendency_loc_q, f->tendency_loc_a,
+                       f->tendency_loc_cld, f->pcovptot, f->prainfrac_toprfz, f->pfsqlf, f->pfsqif,
+                       f->pfcqnng, f->pfcqlng, f->pfsqrf, f->pfsqsf, f->pfcqrng, f->pfcqsng,
+                       f->pfsqltur, f->pfsqitur, f->pfplsl, f->pfplsn, f->pfhpsl, f->pfhpsn};
+  for (const void* q : req)
+    if (!q) return false;
+  return true;
+}
+
+}  // namespace cloudsc_impl
+
+namespace {
+
 template <typename real>
-KArgs<real> make_args(const cloudsc_fields_t* f, int ngptot, int nproma, int klev) {
+KArgs<real> make_args(const cloudsc_fields_t* f, int ngptot, int nproma, int klev, const ParamSet& ps) {
   KArgs<real> a;
   a.pt = (const real*)f->pt; a.pq = (const real*)f->pq;
   a.ttt = (const real*)f->tendency_tmp_t; a.ttq = (const real*)f->tendency_tmp_q;
@@ -124,59 +158,42 @@ KArgs<real> make_args(const cloudsc_fields_t* f, int ngptot, int nproma, int kle
   a.pfcqrng = (real*)f->pfcqrng; a.pfcqsng = (real*)f->pfcqsng; a.pfsqltur = (real*)f->pfsqltur;
   a.pfsqitur = (real*)f->pfsqitur; a.pfplsl = (real*)f->pfplsl; a.pfplsn = (real*)f->pfplsn;
   a.pfhpsl = (real*)f->pfhpsl; a.pfhpsn = (real*)f->pfhpsn;
+  a.par = (const DevParams<real>*)((const char*)ps.dev + (sizeof(real) == 8 ? 0 : kSpOffset));
   a.ngptot = ngptot; a.nproma = nproma; a.klev = klev;
   return a;
 }
 
-
-// the __constant__ mirror of a precision, as a constant-address-space pointer
-template <typename real> __device__ __forceinline__ cptr<DevParams<real>> dev_params();
-template <> __device__ __forceinline__ cptr<DevParams<double>> dev_params<double>() {
-  return (cptr<DevParams<double>>)&g_params_dp;
-}
-template <> __device__ __forceinline__ cptr<DevParams<float>> dev_params<float>() {
-  return (cptr<DevParams<float>>)&g_params_sp;
+// the launch's parameter block, as a constant-address-space pointer (scalar loads)
+template <typename real>
+__device__ __forceinline__ cptr<DevParams<real>> params_of(cptr<KArgs<real>> ka) {
+  return (cptr<DevParams<real>>)((const KArgs<real>*)ka)->par;
 }
 
 }  // namespace
 
-namespace cloudsc_impl {
-bool fields_complete(const cloudsc_fields_t* f) {
-  const void* req[] = {f->pt, f->pq, f->tendency_tmp_t, f->tendency_tmp_q, f->tendency_tmp_a,
-                       f->tendency_tmp_cld, f->pvfl, f->pvfi, f->phrsw, f->phrlw, f->pvervel, f->pap,
-                       f->paph, f->plsm, f->ktype, f->plu, f->psnde, f->pmfu, f->pmfd, f->pa, f->pclv,
-                       f->psupsat, f->plude, f->tendency_loc_t, f->tendency_loc_q, f->tendency_loc_a,
-                       f->tendency_loc_cld, f->pcovptot, f->prainfrac_toprfz, f->pfsqlf, f->pfsqif,
-                       f->pfcqnng, f->pfcqlng, f->pfsqrf, f->pfsqsf, f->pfcqrng, f->pfcqsng,
-                       f->pfsqltur, f->pfsqitur, f->pfplsl, f->pfplsn, f->pfhpsl, f->pfhpsn};
-  for (const void* q : req)
-    if (!q) return false;
-  return true;
-}
-}  // namespace cloudsc_impl
-
 // Kernel entry points.  The KArgs struct is the first explicit kernel argument,
 // i.e. it sits at offset 0 of the kernarg segment; the bodies read it (and the
-// parameter block) through constant-address-space pointers.
+// parameter block it points at) through constant-address-space pointers.
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 __global__ void __launch_bounds__(256, WAVES) kcache_entry(const KArgs<real> a) {
   (void)a;
   libm_tables_to_lds<real>();
-  cloudsc_kcache_body<real, PF, AER, LDSC>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
-                                           dev_params<real>());
+  const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
+  cloudsc_kcache_body<real, PF, AER, LDSC>(ka, params_of<real>(ka));
 }
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 __global__ void __launch_bounds__(256, WAVES) kseg_entry(const KArgs<real> a, const PersistArgs<real> pa) {
   (void)a;
   libm_tables_to_lds<real>();
-  cloudsc_kcache_persistent_body<real, PF, AER, LDSC>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(),
-                                                      dev_params<real>(), pa);
+  const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
+  cloudsc_kcache_persistent_body<real, PF, AER, LDSC>(ka, params_of<real>(ka), pa);
 }
 template <typename real, bool AER>
 __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccScratch<real> s) {
   (void)a;
   libm_tables_to_lds<real>();
-  cloudsc_scc_body<real, AER>((cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr(), s, dev_params<real>());
+  const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
+  cloudsc_scc_body<real, AER>(ka, s, params_of<real>(ka));
 }
 
 // ---------------------------------------------------------------------------
@@ -184,40 +201,51 @@ __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccS
 // ---------------------------------------------------------------------------
 namespace {
 
-template <typename real> int kcache_default_cfg();
-template <> int kcache_default_cfg<double>() { return 20; }    // 2 waves/SIMD, carried state in registers
-// fp32 KCACHE: 3 waves/SIMD with the register prefetch of level k+1; with the
-// double-internal expf/powf it is 2-3 % faster than the 4-wave LDS-carry cfg 140
-// (profiles/r01/sweep_fp32_cfgs_libm.jsonl)
-template <> int kcache_default_cfg<float>() { return 31; }
-template <typename real> int kseg_default_cfg();
-// fp64 KSEG: 2 waves/SIMD, carried state and neighbour planes in registers
-// (cfg 20).  With the streaming I/O it is 1.8 % faster than the LDS-carry cfg
-// 122 (profiles/r01/sweep_kseg_cfgs_nt.jsonl), which had been 5-7 % faster
-// before it (sweep_kseg_ldsc_libm.jsonl).
-template <> int kseg_default_cfg<double>() { return 20; }
-template <> int kseg_default_cfg<float>() { return 31; }      // 3 waves/SIMD, register prefetch
+// Kernel configuration: occupancy target (waves per SIMD, via __launch_bounds__)
+// x load schedule (PF) x where the carried state lives (LDSC).  The product
+// library instantiates only the measured defaults:
+//   fp64: 2 waves/SIMD, carried state and neighbour planes in registers (cfg 20)
+//         -- with the streaming I/O 1.8 % faster than the LDS-carry cfg 122
+//         (profiles/r01/sweep_kseg_cfgs_nt.jsonl);
+//   fp32: 3 waves/SIMD with the register prefetch of level k+1 (cfg 31) -- 2-3 %
+//         faster than the 4-wave LDS-carry cfg 140 (sweep_fp32_cfgs_libm.jsonl).
+// The diagnostic build (-DCLOUDSC_DEBUG_KNOBS, `make variant`) instantiates the
+// whole table and reads CLOUDSC_KCACHE_CFG / CLOUDSC_KSEG_* from the environment
+// (tools/sweep.py); the product library never reads the environment.
+template <typename real> struct DefaultCfg;
+template <> struct DefaultCfg<double> { static constexpr int code = 20, waves = 2, pf = 0; };
+template <> struct DefaultCfg<float> { static constexpr int code = 31, waves = 3, pf = 1; };
 
-
-// kernel configuration code: [1]<waves><pf> -- leading 1 = carried state in LDS
+#ifdef CLOUDSC_DEBUG_KNOBS
+// code: [1]<waves><pf> -- leading 1 = carried state in LDS
 #define CLOUDSC_FOR_EACH_CFG(X) \
   X(10, 1, 0, false) X(11, 1, 1, false) X(20, 2, 0, false) X(21, 2, 1, false) X(30, 3, 0, false) \
-  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) X(122, 2, 2, true) X(130, 3, 0, true) X(132, 3, 2, true) X(22, 2, 2, false) \
-  X(131, 3, 1, true) X(140, 4, 0, true)
+  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) \
+  X(122, 2, 2, true) X(130, 3, 0, true) X(132, 3, 2, true) X(22, 2, 2, false) X(131, 3, 1, true) X(140, 4, 0, true)
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+#endif
 
 template <typename real, bool AER>
-int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma, int cfg) {
-  switch (cfg) {
+int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma) {
+#ifdef CLOUDSC_DEBUG_KNOBS
+  switch (env_int("CLOUDSC_KCACHE_CFG", DefaultCfg<real>::code)) {
 #define X(code, w, pf, ldsc)                                                                                 \
   case code:                                                                                                 \
     hipLaunchKernelGGL((kcache_entry<real, w, pf, AER, ldsc>), dim3(nblocks), dim3(nproma),                  \
                        ldsc ? carry_lds_bytes<real>(nproma) : 0, st, a);                                     \
-    break;
+    return CLOUDSC_OK;
     CLOUDSC_FOR_EACH_CFG(X)
 #undef X
     default: return CLOUDSC_EINVAL;
   }
+#else
+  hipLaunchKernelGGL((kcache_entry<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>), dim3(nblocks),
+                     dim3(nproma), 0, st, a);
   return CLOUDSC_OK;
+#endif
 }
 
 // ---- persistent segmented variant ----
@@ -243,22 +271,16 @@ size_t kseg_scratch_bytes(int nblocks, int nproma) {
 // is short; lower levels also cost more per level) -- the split at NCLDTOP +
 // 60 % of the physics levels (re-tuned with the streaming I/O: 1.768 ms against
 // 1.788 at 62 %, profiles/r01/kseg_bounds_sweep_nt.jsonl); each hand-off costs 19 values out and in plus an
-// L1 invalidate, so fewer segments win once the tail is short.  (Multi-wave
-// workgroups, the earlier NPROMA > 64 form, wanted 8 even segments.)
-int kseg_nseg(int nproma) {
-  (void)nproma;
-  int n = 2;
-  if (const char* e = getenv("CLOUDSC_KSEG_NSEG")) n = atoi(e);
-  return n < 1 ? 1 : (n > kMaxSeg ? kMaxSeg : n);
-}
+// L1 invalidate, so fewer segments win once the tail is short.
+constexpr int kKsegNseg = 2;
+constexpr int kKsegSplitPct = 60;
 
-void kseg_bounds(int nseg, int klev, int ncldtop, int nproma, int* lev) {
+void kseg_bounds(int nseg, int klev, int ncldtop, int* lev) {
   const int top = ncldtop - 1 < klev ? (ncldtop - 1 > 0 ? ncldtop - 1 : 0) : klev;
   const int phys = klev - top;
   lev[0] = 0;
-  (void)nproma;
   if (nseg == 2) {
-    lev[1] = top + (int)((60LL * phys + 50) / 100);
+    lev[1] = top + (int)(((long long)kKsegSplitPct * phys + 50) / 100);
     if (lev[1] <= 0) lev[1] = 1;
     if (lev[1] >= klev) lev[1] = klev - 1;
   } else {
@@ -266,6 +288,30 @@ void kseg_bounds(int nseg, int klev, int ncldtop, int nproma, int* lev) {
   }
   lev[nseg] = klev;
 }
+
+// consumer spin bound of a KSEG hand-off (cloudsc_debug_set_kseg_spin_limit)
+std::atomic<unsigned> g_kseg_spin_limit{1u << 24};
+// schedule overrides for the tests of the hand-off (cloudsc_debug_set_kseg_schedule); 0 = default
+std::atomic<int> g_kseg_nseg{0}, g_kseg_grid{0};
+
+}  // namespace
+
+// KSEG workspace words: [0] dequeue counter, [1] timed-out hand-offs (sticky:
+// accumulated over launches until cloudsc_gpu_check reads and clears it),
+// [2] a tag marking [1] as initialised, [64..] per-sub-block flags.  Every
+// launch zeroes the counter and the flags; the first launch on a workspace
+// (tag absent) also zeroes the error word.
+constexpr unsigned kKsegTag = 0xC105D5C1u;
+__global__ void __launch_bounds__(256) kseg_prepare_kernel(unsigned* ws, int nflags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    ws[0] = 0u;
+    if (ws[2] != kKsegTag) { ws[1] = 0u; ws[2] = kKsegTag; }
+  }
+  for (int j = i; j < nflags; j += gridDim.x * blockDim.x) ws[64 + j] = 0u;
+}
+
+namespace {
 
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
@@ -288,63 +334,66 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
     ncu = 256;
   int grid = per_cu * ncu;
-  if (const char* e = getenv("CLOUDSC_KSEG_GRID")) grid = atoi(e) > 0 ? atoi(e) : grid;
+  if (const int g = g_kseg_grid.load(std::memory_order_relaxed)) grid = g;
+#ifdef CLOUDSC_DEBUG_KNOBS
+  grid = env_int("CLOUDSC_KSEG_GRID", 0) > 0 ? env_int("CLOUDSC_KSEG_GRID", 0) : grid;
+#endif
   if (grid > nitems) grid = nitems;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, st, a, pa);
   return CLOUDSC_OK;
 }
 
 template <typename real, bool AER>
-int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
-                int cfg) {
-  switch (cfg) {
+int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
+#ifdef CLOUDSC_DEBUG_KNOBS
+  switch (env_int("CLOUDSC_KCACHE_CFG", DefaultCfg<real>::code)) {
 #define X(code, w, pf, ldsc) \
   case code: return launch_kseg_cfg<real, w, pf, AER, ldsc>(st, a, pa, nproma, nitems);
     CLOUDSC_FOR_EACH_CFG(X)
 #undef X
     default: return CLOUDSC_EINVAL;
   }
+#else
+  return launch_kseg_cfg<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>(st, a, pa, nproma, nitems);
+#endif
 }
 
 template <typename real>
-int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
-           void* scratch, const void* plude_in) {
-  KArgs<real> a = make_args<real>(f, ngptot, nproma, klev);
+int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
+           void* scratch, const void* plude_in, const ParamSet& ps) {
+  KArgs<real> a = make_args<real>(f, ngptot, nproma, klev, ps);
   if (plude_in) a.plude_in = (const real*)plude_in;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
-  const bool aer = g_aer[device];
+  const bool aer = ps.aer;
   if (aer && (!f->pre_ice || !f->picrit_aer || !f->pnice)) return CLOUDSC_EINVAL;
   int rc = CLOUDSC_OK;
   if (variant == CLOUDSC_VARIANT_KCACHE) {
-    // kernel configuration (occupancy target x load schedule); the default is
-    // the measured best, CLOUDSC_KCACHE_CFG=<waves><pf> overrides it for experiments
-    int cfg = kcache_default_cfg<real>();
-    if (const char* e = getenv("CLOUDSC_KCACHE_CFG")) cfg = atoi(e);
-    rc = aer ? launch_kcache<real, true>(st, a, nblocks, nproma, cfg)
-             : launch_kcache<real, false>(st, a, nblocks, nproma, cfg);
+    rc = aer ? launch_kcache<real, true>(st, a, nblocks, nproma) : launch_kcache<real, false>(st, a, nblocks, nproma);
   } else if (variant == CLOUDSC_VARIANT_KSEG) {
     if (!scratch) return CLOUDSC_EINVAL;
-    int cfg = kseg_default_cfg<real>();
-    if (const char* e = getenv("CLOUDSC_KCACHE_CFG")) cfg = atoi(e);
-    const int ncldtop = g_ncldtop[device];
     PersistArgs<real> pa;
     pa.counter = (unsigned*)scratch;
     pa.err = (unsigned*)scratch + 1;
     pa.flags = (unsigned*)((char*)scratch + 256);
     pa.state = (real*)((char*)scratch + kseg_ctl_bytes(nblocks, nproma));
     pa.nsub = kseg_nsub(nproma);
-    // item order (segment, block, sub-block); CLOUDSC_KSEG_SBMAJOR=1 runs
-    // (segment, sub-block, block) instead -- the same within noise at NPROMA 128,
-    // 2 % slower at 256 (profiles/r01/kseg_subblock_order.jsonl)
+    pa.spin_limit = g_kseg_spin_limit.load(std::memory_order_relaxed);
+    // item order (segment, block, sub-block); (segment, sub-block, block) measured
+    // the same within noise at NPROMA 128, 2 % slower at 256 (profiles/r01/kseg_subblock_order.jsonl)
     pa.sb_major = 0;
-    if (const char* e = getenv("CLOUDSC_KSEG_SBMAJOR")) pa.sb_major = atoi(e) != 0;
-    pa.nseg = kseg_nseg(nproma);
+    pa.nseg = kKsegNseg;
+    if (const int n = g_kseg_nseg.load(std::memory_order_relaxed)) pa.nseg = n > kMaxSeg ? kMaxSeg : n;
+#ifdef CLOUDSC_DEBUG_KNOBS
+    pa.sb_major = env_int("CLOUDSC_KSEG_SBMAJOR", 0) != 0;
+    pa.nseg = env_int("CLOUDSC_KSEG_NSEG", kKsegNseg);
+    pa.nseg = pa.nseg < 1 ? 1 : (pa.nseg > kMaxSeg ? kMaxSeg : pa.nseg);
+#endif
     if (pa.nseg > klev) pa.nseg = klev;
     pa.nblocks = nblocks;
-    pa.nitems = pa.nseg * nblocks * pa.nsub;
     for (int q = 0; q <= kMaxSeg; q++) pa.lev[q] = klev;
-    kseg_bounds(pa.nseg, klev, ncldtop, nproma, pa.lev);
-    if (const char* e = getenv("CLOUDSC_KSEG_BOUNDS")) {   // experiments: explicit interior boundaries
+    kseg_bounds(pa.nseg, klev, ps.ncldtop, pa.lev);
+#ifdef CLOUDSC_DEBUG_KNOBS
+    if (const char* e = getenv("CLOUDSC_KSEG_BOUNDS")) {   // explicit interior boundaries
       int n = 1, v = 0;
       const char* q = e;
       while (*q && n < kMaxSeg) {
@@ -355,11 +404,15 @@ int launch(int device, hipStream_t st, int variant, const cloudsc_fields_t* f, i
       }
       pa.nseg = n;
       pa.lev[n] = klev;
-      pa.nitems = pa.nseg * nblocks * pa.nsub;
     }
-    HIPCHK(hipMemsetAsync(scratch, 0, kseg_ctl_bytes(nblocks, nproma), st));
-    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, cfg)
-             : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, cfg);
+#endif
+    pa.nitems = pa.nseg * nblocks * pa.nsub;
+    {
+      const int nflags = nblocks * pa.nsub;
+      const int g = (nflags + 255) / 256 < 64 ? (nflags + 255) / 256 : 64;
+      hipLaunchKernelGGL(kseg_prepare_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, (unsigned*)scratch, nflags);
+    }
+    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems) : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems);
   } else {
     if (!scratch) return CLOUDSC_EINVAL;
     SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
@@ -394,15 +447,11 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t* params) {
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n || device >= kMaxDevices)
     return CLOUDSC_ENODEV;
   HIPCHK(hipSetDevice(device));
-  const DevParams<double> dp = fold_params<double>(*params);
-  const DevParams<float> sp = fold_params<float>(*params);
-  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_params_dp), &dp, sizeof(dp)));
-  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_params_sp), &sp, sizeof(sp)));
+  // The default set is overwritten in place: wait for every launch on the
+  // device that may still read it (states and pipelines have their own sets).
   HIPCHK(hipDeviceSynchronize());
-  g_aer[device] = params->laericesed || params->laericeauto;
-  g_ncldtop[device] = params->ncldtop;
-  g_inited[device] = true;
-  return CLOUDSC_OK;
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  return param_set_upload(&g_default[device], device, params);
 }
 
 long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev) {
@@ -432,21 +481,40 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
   // 64-column sub-blocks of any block width
   const int max_nproma = variant == CLOUDSC_VARIANT_KSEG ? (1 << 24) : 256;
   if (ngptot <= 0 || nproma <= 0 || nproma > max_nproma || klev < 2) return CLOUDSC_EINVAL;
-  if (!g_inited[device]) return CLOUDSC_ENOINIT;
   return CLOUDSC_OK;
 }
 
 // plude_in: NULL = in place (the reference INOUT semantics); otherwise the
-// values of plude are read from there and the results written to f->plude
+// values of plude are read from there and the results written to f->plude.
+// ps: the parameter set of the launch (NULL = the device's default set).
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
-                 const cloudsc_fields_t* f, void* scratch, const void* plude_in) {
+                 const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps) {
   int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
   if (rc) return rc;
+  if (!ps) ps = device_default_params(device);
+  if (!ps || !ps->dev) return CLOUDSC_ENOINIT;
+  if (ps->device != device) return CLOUDSC_EINVAL;
   if (!f || !fields_complete(f)) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
-  return precision == CLOUDSC_FP64 ? launch<double>(device, st, variant, f, ngptot, nproma, klev, scratch, plude_in)
-                                   : launch<float>(device, st, variant, f, ngptot, nproma, klev, scratch, plude_in);
+  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps)
+                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps);
+}
+
+int kseg_check(int device, void* stream, void* scratch) {
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  unsigned w[3] = {0, 0, 0};
+  HIPCHK(hipMemcpy(w, scratch, sizeof(w), hipMemcpyDeviceToHost));
+  const unsigned err = w[2] == kKsegTag ? w[1] : 0u;   // no tag: no KSEG launch on this workspace yet
+  if (err) {
+    HIPCHK(hipMemset((unsigned*)scratch + 1, 0, sizeof(unsigned)));
+    char msg[96];
+    std::snprintf(msg, sizeof(msg), "KSEG: %u segment hand-offs timed out", err);
+    set_error_text(msg);
+    return CLOUDSC_EHANDOFF;
+  }
+  return CLOUDSC_OK;
 }
 }  // namespace cloudsc_impl
 
@@ -454,7 +522,32 @@ extern "C" {
 
 int cloudsc_gpu_run(int device, void* stream, int precision, int variant, int ngptot, int nproma,
                     int klev, const cloudsc_fields_t* f, void* scratch) {
-  return gpu_run_impl(device, stream, precision, variant, ngptot, nproma, klev, f, scratch, nullptr);
+  return gpu_run_impl(device, stream, precision, variant, ngptot, nproma, klev, f, scratch, nullptr, nullptr);
+}
+
+int cloudsc_gpu_check(int device, void* stream, int variant, void* scratch) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CLOUDSC_ENODEV;
+  if (variant != CLOUDSC_VARIANT_KSEG) {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    return CLOUDSC_OK;
+  }
+  if (!scratch) return CLOUDSC_EINVAL;
+  return kseg_check(device, stream, scratch);
+}
+
+int cloudsc_debug_set_kseg_schedule(int nseg, int grid) {
+  if (nseg < 0 || grid < 0) return CLOUDSC_EINVAL;
+  g_kseg_nseg.store(nseg, std::memory_order_relaxed);
+  g_kseg_grid.store(grid, std::memory_order_relaxed);
+  return CLOUDSC_OK;
+}
+
+int cloudsc_debug_set_kseg_spin_limit(long long limit) {
+  if (limit < 0) limit = 1LL << 24;
+  g_kseg_spin_limit.store(limit > 0xffffffffLL ? 0xffffffffu : (unsigned)limit, std::memory_order_relaxed);
+  return CLOUDSC_OK;
 }
 
 const char* cloudsc_strerror(int code) {
@@ -466,6 +559,7 @@ const char* cloudsc_strerror(int code) {
     case CLOUDSC_ENOINIT: return "cloudsc_gpu_init not called for this device";
     case CLOUDSC_ENOMEM: return "out of memory";
     case CLOUDSC_EIO: return "I/O error";
+    case CLOUDSC_EHANDOFF: return "KSEG segment hand-off timed out (outputs invalid)";
     default: return "unknown error";
   }
 }
@@ -493,4 +587,3 @@ long long cloudsc_abi_sizeof(int which) {
 }
 
 }  // extern "C"
-

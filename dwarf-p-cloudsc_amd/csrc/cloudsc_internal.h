@@ -10,6 +10,24 @@ namespace cloudsc_impl {
 
 constexpr int kMaxDevices = 64;
 
+// One parameter set on one device: the host-folded fp64 and fp32 DevParams
+// blocks in device memory (read by the kernels through a KArgs pointer), plus
+// the host-side values the launch itself needs.
+struct ParamSet {
+  void* dev = nullptr;     // device block (fp64 mirror at 0, fp32 mirror after it)
+  int device = -1;
+  bool aer = false;        // LAERICESED || LAERICEAUTO: aerosol inputs are read
+  int ncldtop = 0;         // NCLDTOP (KSEG segment bounds)
+};
+int check_params(const cloudsc_params_t* p);
+// (re)upload `p` into ps (allocated on first use) on `device`; synchronous
+int param_set_upload(ParamSet* ps, int device, const cloudsc_params_t* p);
+// copy of another set on the same device (device-to-device)
+int param_set_copy(ParamSet* dst, const ParamSet* src);
+void param_set_free(ParamSet* ps);
+// the device's default set (cloudsc_gpu_init), NULL if never initialised
+const ParamSet* device_default_params(int device);
+
 // records "what: hip error string" for cloudsc_last_hip_error(); returns CLOUDSC_EHIP
 int hip_fail(hipError_t e, const char* what);
 // sets the cloudsc_last_hip_error() text for a failure that is not a HIP error
@@ -19,8 +37,12 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
 // every pointer the kernel reads or writes (aerosol inputs excepted) is set
 bool fields_complete(const cloudsc_fields_t* f);
 // cloudsc_gpu_run with an optional separate source of plude (NULL = in place)
+// and an explicit parameter set (NULL = the device's default set)
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
-                 const cloudsc_fields_t* f, void* scratch, const void* plude_in);
+                 const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps);
+// waits for `stream` and returns CLOUDSC_EHANDOFF if the last KSEG launch on
+// `scratch` counted a timed-out segment hand-off
+int kseg_check(int device, void* stream, void* scratch);
 
 }  // namespace cloudsc_impl
 

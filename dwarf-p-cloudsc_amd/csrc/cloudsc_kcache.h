@@ -27,23 +27,7 @@
 // fp64 output is the reference kernel's, bit for bit.
 #pragma once
 #include "cloudsc_dev.h"
-#ifdef CLOUDSC_BRANCH_STATS
-// diagnostic build only: count the waves that enter each branch body
-__device__ unsigned long long g_branch_count[32];
-#define CLOUDSC_BRANCH_COUNT(id)                                                         \
-  do {                                                                                 \
-    const unsigned long long m_ = __ballot(1);                                         \
-    if ((int)__lane_id() == __ffsll((long long)m_) - 1) atomicAdd(&g_branch_count[id], 1ull); \
-  } while (0)
-#else
-#define CLOUDSC_BRANCH_COUNT(id) do {} while (0)
-#endif
-#ifdef CLOUDSC_CONST_PARAMS
-#include CLOUDSC_CONST_PARAMS   // experiment: parameters as compile-time constants
-#define CLOUDSC_PARAMS_HERE const ConstParams<real> c{}
-#else
 #define CLOUDSC_PARAMS_HERE const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar)
-#endif
 
 namespace cloudsc {
 
@@ -57,6 +41,7 @@ struct KArgs {
   real *plude, *tlt, *tlq, *tla, *tlcld, *pcovptot, *prainfrac;
   real *pfsqlf, *pfsqif, *pfcqnng, *pfcqlng, *pfsqrf, *pfsqsf, *pfcqrng, *pfcqsng;
   real *pfsqltur, *pfsqitur, *pfplsl, *pfplsn, *pfhpsl, *pfhpsn;
+  const DevParams<real>* par;   // the launch's parameter set (device memory, read with scalar loads)
   int ngptot, nproma, klev;
 };
 
@@ -66,36 +51,27 @@ enum { QL = 0, QI = 1, QR = 2, QS = 3, QV = 4 };
 // pointer) + the lane's byte offset (one shared 32-bit VGPR).  This is the
 // global_load/store "saddr" form: no per-field 64-bit VGPR pointers.
 template <typename T>
-__device__ __forceinline__ T ldg(const T* ubase, size_t uidx, unsigned lane_bytes) {
+CLOUDSC_HD T ldg(const T* ubase, size_t uidx, unsigned lane_bytes) {
   return *(const T*)((const char*)(ubase + uidx) + lane_bytes);
 }
 // Outputs are written once and never read back by the kernel, and the level
 // inputs are read once: both go as non-temporal (streaming) accesses, so the
 // caches keep what is re-read (the neighbour levels, the hand-off state).
-// -1.9 % kernel time on the same box (profiles/r01/ab_nontemporal.txt);
-// CLOUDSC_CACHED_IO restores plain accesses.  stg_cached is for scratch that
-// is read back (the SCC variant's temporaries).
+// -1.9 % kernel time on the same box (profiles/r01/ab_nontemporal.txt).
+// stg_cached is for scratch that is read back (the SCC variant's temporaries).
 template <typename T>
-__device__ __forceinline__ void stg_cached(T* ubase, size_t uidx, unsigned lane_bytes,
+CLOUDSC_HD void stg_cached(T* ubase, size_t uidx, unsigned lane_bytes,
                                            typename std::common_type<T>::type v) {
   *(T*)((char*)(ubase + uidx) + lane_bytes) = v;
 }
 template <typename T>
-__device__ __forceinline__ void stg(T* ubase, size_t uidx, unsigned lane_bytes, typename std::common_type<T>::type v) {
-#ifndef CLOUDSC_CACHED_IO
+CLOUDSC_HD void stg(T* ubase, size_t uidx, unsigned lane_bytes, typename std::common_type<T>::type v) {
   __builtin_nontemporal_store(v, (T*)((char*)(ubase + uidx) + lane_bytes));
-#else
-  stg_cached(ubase, uidx, lane_bytes, v);
-#endif
 }
 // a level input, read exactly once
 template <typename T>
-__device__ __forceinline__ T ldg1(const T* ubase, size_t uidx, unsigned lane_bytes) {
-#ifndef CLOUDSC_CACHED_IO
+CLOUDSC_HD T ldg1(const T* ubase, size_t uidx, unsigned lane_bytes) {
   return __builtin_nontemporal_load((const T*)((const char*)(ubase + uidx) + lane_bytes));
-#else
-  return ldg(ubase, uidx, lane_bytes);
-#endif
 }
 
 // Per-level inputs of one column (the prefetch unit).
@@ -191,7 +167,7 @@ struct PhysOut {
 // every level): branches around memory operations make hipcc's vmcnt
 // bookkeeping fall back to vmcnt(0), which drains the software pipeline.
 template <typename real, bool AER>
-__device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& A, size_t u2, size_t u3, int k,
+CLOUDSC_HD void load_level(LevelIn<real>& L, const KArgs<real>& A, size_t u2, size_t u3, int k,
                                            int klev, int nproma, unsigned lo) {
   const size_t i = u2 + (size_t)k * nproma;
   L.pt = ldg1(A.pt, i, lo); L.pq = ldg1(A.pq, i, lo); L.ttt = ldg1(A.ttt, i, lo); L.ttq = ldg1(A.ttq, i, lo);
@@ -214,7 +190,7 @@ __device__ __forceinline__ void load_level(LevelIn<real>& L, const KArgs<real>& 
 
 // ===== 1. initial values, tidy-up, FOEALFA at one level (cloudsc_c.c:462-575, 588, 625) =====
 template <typename real, typename P>
-__device__ __forceinline__ void init_level(const P& c, const LevelIn<real>& in, LevelState<real>& s) {
+CLOUDSC_HD void init_level(const P& c, const LevelIn<real>& in, LevelState<real>& s) {
   s.ztp1 = in.pt + c.ptsphy * in.ttt;
   real* zqx = s.zqx;
   real* zlneg = s.zlneg;
@@ -271,7 +247,7 @@ __device__ __forceinline__ void init_level(const P& c, const LevelIn<real>& in, 
 
 // ===== 3.-6. physics of one level ncldtop <= k (cloudsc_c.c:732-2508) =====
 template <typename real, typename P, typename CS>
-__device__ __forceinline__ void physics_level(const P& c, const int k, const int klev,
+CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
                                               const int ncldtop0, const LevelIn<real>& in,
                                               const Neighbors<real>& nb, const ColConst<real>& cc,
                                               LevelState<real>& ls, CS& cs, PhysOut<real>& po) {
@@ -288,7 +264,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
   real* ctend = po.ctend;
   real& plude_k = po.plude_k;
   real& atend = po.atend;
-  CLOUDSC_BRANCH_COUNT(31);
+
     const real pap_k = in.pap;
     // saturation values (:583-609)
     const real e_liq = exp_liq<real>(c, ztp1), e_ice = exp_ice<real>(c, ztp1);
@@ -371,13 +347,13 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       zsupsat = fmax(cl_div(((R(1.0) - za) * (zqp1env - zfac * zqsice)), zcorqsice), R(0.0));
     }
     const bool warm_homo = ztp1 > c.rthomo;
-    if (zsupsat > zepsec) { CLOUDSC_BRANCH_COUNT(0);
+    if (zsupsat > zepsec) {
       if (warm_homo) { sa_lv = sa_lv - zsupsat; zqxfg[QL] = zqxfg[QL] + zsupsat;
       } else { sa_iv = sa_iv - zsupsat; zqxfg[QI] = zqxfg[QI] + zsupsat;
       }
       zsolac = (R(1.0) - za) * zfaci;
     }
-    if (in.psupsat > zepsec) { CLOUDSC_BRANCH_COUNT(1);
+    if (in.psupsat > zepsec) {
       if (warm_homo) {
         sa_ll = sa_ll + in.psupsat; psup_l = in.psupsat; zqxfg[QL] = zqxfg[QL] + in.psupsat;
       } else {
@@ -442,7 +418,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 
     // 3.4 erosion of clouds by turbulent mixing (:1087-1118)
     const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? sval(c.zldifdt_conv) : sval(c.zldifdt0);
-    if (zli > zepsec) { CLOUDSC_BRANCH_COUNT(2);
+    if (zli > zepsec) {
       const real ze = zldifdt * fmax(zqsmix - zqx[QV], R(0.0));
       real zleros = za * ze;
       zleros = fmin(zleros, zevaplimmix);
@@ -467,14 +443,8 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       real tt = fmax(ztp1 + zdtforc, R(160.0));
       real qsm = zqsmix;
       const real zqp = cl_div(R(1.0), pap_k);
-#ifdef CLOUDSC_ABLATE_NEWTON   // timing-only diagnostic build: the two Newton steps replaced by a cheap stand-in
-      tt = launder_vgpr(tt); qsm = qsm - R(1e-9) * tt * zqp;
-  #pragma unroll
-      for (int it = 0; it < 0; it++) {
-#else
   #pragma unroll
       for (int it = 0; it < 2; it++) {
-#endif
         const real a = foealfa<real>(c, tt);
         real zqsat = (c.r2es * (a * exp_liq<real>(c, tt) + (R(1.0) - a) * exp_ice<real>(c, tt))) * zqp;
         zqsat = fmin(R(0.5), zqsat);
@@ -488,7 +458,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     }
 
     // 3.4a evaporation of clouds (:1189-1207)
-    if (zdqs > R(0.0)) { CLOUDSC_BRANCH_COUNT(3);
+    if (zdqs > R(0.0)) {
       real zlevap = za * fmin(zdqs, zlicld);
       zlevap = fmin(zlevap, zevaplimmix);
       zlevap = fmin(zlevap, fmax(zqsmix - zqx[QV], R(0.0)));
@@ -496,7 +466,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       sa_iv = sa_iv + zicefrac * zlevap;
     }
     // 3.4b(1) increase of cloud water in existing clouds (:1213-1250)
-    if (zdqs <= -c.rlmin && za > zepsec) { CLOUDSC_BRANCH_COUNT(4);
+    if (zdqs <= -c.rlmin && za > zepsec) {
       real zlcond1 = fmax(-zdqs, R(0.0));
       real zcdmax;
       if (za > R(0.99)) {
@@ -513,7 +483,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       }
     }
     // 3.4b(2) generation of new clouds (:1253-1363)
-    if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) { CLOUDSC_BRANCH_COUNT(5);
+    if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) {
       real zrhc = c.ramid;
       const real zsigk = cl_div(pap_k, cc.paph_sfc);
       if (zsigk > R(0.8)) {
@@ -530,7 +500,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
         zqe = zqx[QV] + zli;
       }
       const real zfacn = (c.nssopt == 0 || ztp1 >= c.rtt) ? R(1.0) : zfokoop;
-      if (zqe >= zqsice * zfacn * zrhc && zqe < zqsice * zfacn) { CLOUDSC_BRANCH_COUNT(6);
+      if (zqe >= zqsice * zfacn * zrhc && zqe < zqsice * zfacn) {
         real zacond = cl_div(-((R(1.0) - za) * zfacn) * zdqs, fmax(R(2.0) * (zfacn * zqsice - zqe), zepsec));
         zacond = fmin(zacond, R(1.0) - za);
         real zlcond2 = -(zfacn * zdqs) * R(0.5) * zacond;
@@ -555,7 +525,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // 3.7 growth of ice by vapour deposition, Rotstayn (:1382-1447)
     if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
     else cs.zcldtopdist = cs.zcldtopdist + cl_div(zdp, (zrho * c.rg));
-    if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) { CLOUDSC_BRANCH_COUNT(7);
+    if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
       const real zvpice = cl_div(((c.r2es * e_ice) * c.rv), c.rd);
       const real zvpliq = zvpice * zfokoop;
       const real zicenuclei = R(1000.0) * cl_exp<real>(cl_div((R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
@@ -591,7 +561,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 
     // precip cover overlap, MAX-RAN (:1594-1611)
     real zcovpclr, zraincld, zsnowcld;
-    if (zqpretot > zepsec) { CLOUDSC_BRANCH_COUNT(8);
+    if (zqpretot > zepsec) {
       cs.zcovptot = R(1.0) - cl_div((R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)), (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6))));
       cs.zcovptot = fmax(cs.zcovptot, c.rcovpmin);
       zcovpclr = fmax(R(0.0), cs.zcovptot - za);
@@ -604,7 +574,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 
     const bool cold = ztp1 <= c.rtt;
     // 4.3a autoconversion to snow (:1616-1637)
-    if (cold && zicecld > zepsec) { CLOUDSC_BRANCH_COUNT(9);
+    if (cold && zicecld > zepsec) {
       real zzco = c.zzco_snow * cl_exp<real>(c.rsnowlin2 * (ztp1 - c.rtt));
       real zlcrit = sval(c.rlcritsnow);
       if (c.laericeauto) {
@@ -615,9 +585,9 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       sb_is = sb_is + zzco * (R(1.0) - cl_exp<real>(-(r * r)));
     }
     // 4.3b warm rain, Khairoutdinov and Kogan 2000 (:1644-1761)
-    if (zliqcld > zepsec) { CLOUDSC_BRANCH_COUNT(10);
+    if (zliqcld > zepsec) {
       real zrainaut = R(0.0), zrainacc = R(0.0);
-      if (zliqcld > cc.kk_lcrit) { CLOUDSC_BRANCH_COUNT(11);
+      if (zliqcld > cc.kk_lcrit) {
         zrainaut = ((((R(1.5) * za) * c.ptsphy) * c.rcl_kkaau) * cl_pow<real>(zliqcld, c.rcl_kkbauq)) * cc.kk_pow;
         zrainaut = fmin(zrainaut, zqxfg[QL]);
         if (zrainaut < zepsec) zrainaut = R(0.0);
@@ -632,7 +602,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       }
     }
     // riming of snow by cloud water (:1768-1808)
-    if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) { CLOUDSC_BRANCH_COUNT(12);
+    if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) {
       const real zfallcorr = cl_pow<real>(cl_div(c.rdensref, zrho), R(0.4));
       real zsnowrime = ((((R(0.3) * cs.zcovptot) * c.ptsphy) * c.rcl_const7s) * zfallcorr) *
                        cl_pow<real>((zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
@@ -642,7 +612,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 
     // 4.4a melting of snow and ice (:1817-1859)
     const real zicetot = zqxfg[QI] + zqxfg[QS];
-    if (zicetot > zepsec && ztp1 > c.rtt) { CLOUDSC_BRANCH_COUNT(13);
+    if (zicetot > zepsec && ztp1 > c.rtt) {
       const real zsubsat = fmax(zqsice - zqx[QV], R(0.0));
       const real ztdmtw0 = ztp1 - c.rtt - zsubsat * (ztw1 + ztw2 * (pap_k - ztw3) - ztw4 * (ztp1 - ztw5));
       const real zcons1 = fabs(cl_div((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)), c.rtaumel));
@@ -664,7 +634,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     }
 
     // 4.4b freezing of rain (:1864-1908)
-    if (zqx[QR] > zepsec) { CLOUDSC_BRANCH_COUNT(14);
+    if (zqx[QR] > zepsec) {
       if (cold && cs.t_prev > c.rtt) {
         const real tot = fmax(zqx[QS] + zqx[QR], zepsec);
         cs.rainfrac = cl_div(zqx[QR], tot);
@@ -688,7 +658,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // 4.4c freezing of liquid (:1913-1928)
     {
       const real zfrzmax = fmax((c.rthomo - ztp1) * c.zrldcp, R(0.0));
-      if (zfrzmax > zepsec && zqxfg[QL] > zepsec) { CLOUDSC_BRANCH_COUNT(15);
+      if (zfrzmax > zepsec && zqxfg[QL] > zepsec) {
         const real zfrz = fmin(zqxfg[QL], zfrzmax);
         sa_li = sa_li + zfrz;
       }
@@ -700,7 +670,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     {
       const real zzrh = fmin(R(0.8), zzrh0);
       const real zqe = fmax(R(0.0), fmin(zqx[QV], zqsliq));
-      if (zcovpclr > zepsec && zqxfg[QR] > zepsec && zqe < zzrh * zqsliq) { CLOUDSC_BRANCH_COUNT(16);
+      if (zcovpclr > zepsec && zqxfg[QR] > zepsec && zqe < zzrh * zqsliq) {
         const real zpreclr = cl_div(zqxfg[QR], cs.zcovptot);
         const real zfallcorr = cl_pow<real>(cl_div(c.rdensref, zrho), R(0.4));
         const real zesatliq = c.rv_rd * (c.r2es * e_liq);
@@ -723,7 +693,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       const real zzrh = zzrh0;
       real zqe = cl_div((zqx[QV] - za * zqsice), fmax(zepsec, R(1.0) - za));
       zqe = fmax(R(0.0), fmin(zqe, zqsice));
-      if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) { CLOUDSC_BRANCH_COUNT(17);
+      if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) {
         const real x = cs.zcovptot * zdtgdp;
         const real zpreclr = cl_div((zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
         const real zbeta1 = cl_div(((cl_div(sqrt(cl_div(pap_k, cc.paph_sfc)), c.rvrfactor)) * zpreclr), fmax(zcovpclr, zepsec));
@@ -754,7 +724,6 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
     // zsolqa[n][m] and its transpose zsolqa[m][n] (the diagonal twice).
     // The structurally-zero entries are kept as literal zeros so the
     // summation order (and hence rounding) matches the dense reference.
-#ifndef CLOUDSC_ABLATE_SINKS   // timing-only diagnostic build: no sink truncation (5.2)
     {
       real z = R(0.0), psum, zrat;
       // m = ql: zsolqa[n][ql] = {ll, il, rl, sl, vl}
@@ -795,7 +764,6 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
       if (sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
       if (sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
     }
-#endif
 
     // 5.2.2 implicit solver (:2294-2397).  With the zsolqb sparsity above,
     //   zqlhs = I + diag(fallsink) + diag(row sums of zsolqb) - offdiag(zsolqb)
@@ -873,7 +841,7 @@ __device__ __forceinline__ void physics_level(const P& c, const int k, const int
 
 // ===== 8. flux diagnostics of one level (cloudsc_c.c:2521-2582), written at half level k+1 =====
 template <typename real, typename P, typename CS>
-__device__ __forceinline__ void flux_level(const P& c, const KArgs<real>& A, size_t h, unsigned lo,
+CLOUDSC_HD void flux_level(const P& c, const KArgs<real>& A, size_t h, unsigned lo,
                                            const LevelIn<real>& in, const LevelState<real>& ls,
                                            const PhysOut<real>& po, real paph_k, real paph_n,
                                            CS& cs) {
@@ -905,7 +873,7 @@ __device__ __forceinline__ void flux_level(const P& c, const KArgs<real>& A, siz
 
 // level-0 half-level outputs (cloudsc_c.c:2523-2543, 2578-2579)
 template <typename real, typename P>
-__device__ __forceinline__ void flux_top(const P& c, const KArgs<real>& A, size_t h0, unsigned lo) {
+CLOUDSC_HD void flux_top(const P& c, const KArgs<real>& A, size_t h0, unsigned lo) {
   stg(A.pfsqlf, h0, lo, R(0.0)); stg(A.pfsqif, h0, lo, R(0.0)); stg(A.pfsqrf, h0, lo, R(0.0));
   stg(A.pfsqsf, h0, lo, R(0.0)); stg(A.pfcqlng, h0, lo, R(0.0)); stg(A.pfcqnng, h0, lo, R(0.0));
   stg(A.pfcqrng, h0, lo, R(0.0)); stg(A.pfcqsng, h0, lo, R(0.0));
@@ -916,7 +884,7 @@ __device__ __forceinline__ void flux_top(const P& c, const KArgs<real>& A, size_
 }
 
 template <typename real, typename P>
-__device__ __forceinline__ ColConst<real> column_constants(const P& c, const KArgs<real>& A,
+CLOUDSC_HD ColConst<real> column_constants(const P& c, const KArgs<real>& A,
                                                            size_t u1, size_t uh, unsigned lo) {
   ColConst<real> cc;
   const real plsm = ldg(A.plsm, u1, lo);
@@ -930,7 +898,7 @@ __device__ __forceinline__ ColConst<real> column_constants(const P& c, const KAr
 }
 
 template <typename real>
-__device__ __forceinline__ void store_level(const KArgs<real>& A, size_t u2, size_t u3, int k, int klev,
+CLOUDSC_HD void store_level(const KArgs<real>& A, size_t u2, size_t u3, int k, int klev,
                                             int nproma, unsigned lo, bool physics, const LevelState<real>& ls,
                                             const PhysOut<real>& po) {
   const size_t i = u2 + (size_t)k * nproma;
@@ -945,7 +913,7 @@ __device__ __forceinline__ void store_level(const KArgs<real>& A, size_t u2, siz
 }
 
 template <typename real, typename CS>
-__device__ __forceinline__ void init_carry(CS& cs) {
+CLOUDSC_HD void init_carry(CS& cs) {
   cs.t_prev = cs.a_prev = cs.pap_prev = R(0.0);
   cs.zanewm1 = cs.zcovptot = cs.zcovpmax = cs.zcldtopdist = cs.rainfrac = R(0.0);
   cs.qxnm1_l = cs.qxnm1_i = R(0.0);
@@ -1115,6 +1083,7 @@ struct PersistArgs {
   int nseg, nitems, nblocks;
   int nsub;               // 64-column sub-blocks per NPROMA block (one wave each)
   int sb_major;           // item order (segment, sub-block, block) instead of (segment, block, sub-block)
+  unsigned spin_limit;    // polls before a consumer gives up (and counts an error)
   int lev[kMaxSeg + 1];
 };
 
@@ -1195,18 +1164,16 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       // wait, barrier, plain loads
       if (wave0) {
         for (unsigned spins = 0;; spins++) {
-          const unsigned f = __builtin_amdgcn_readfirstlane(
-              __hip_atomic_load(P.flags + sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          if (f >= (unsigned)seg) break;
-          if (spins > (1u << 24)) {                      // bounded: never hang
+          if (spins >= P.spin_limit) {                   // bounded: never hang; the host reports it
             __hip_atomic_fetch_add(P.err, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
+          const unsigned f = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(P.flags + sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          if (f >= (unsigned)seg) break;
           __builtin_amdgcn_s_sleep(4);
         }
-#ifndef CLOUDSC_KSEG_NO_ACQUIRE   // timing-only diagnostic build (unsynchronised: wrong in general)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();

@@ -70,6 +70,7 @@ struct cloudsc_host_pipeline {
   };
   std::vector<Slot> slots;
   std::vector<void*> allocs;
+  ParamSet params;          // snapshot of the device's default set at creation
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -93,6 +94,9 @@ int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int 
   p->host = *host;
   auto fail = [&](int r) { cloudsc_host_pipeline_destroy(p); return r; };
   if (hipSetDevice(device) != hipSuccess) return fail(CLOUDSC_ENODEV);
+  // the pipeline runs with the parameters current at creation, whatever a
+  // later cloudsc_gpu_init does to the device's default set
+  if ((rc = param_set_copy(&p->params, device_default_params(device)))) return fail(rc);
   void* const* hf = (void* const*)&p->host;
   // pin the caller's arrays in place (already-pinned memory is fine)
   for (int i = 0; i < kNumFields; i++) {
@@ -166,7 +170,8 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
       HIPCHK(hipMemcpyAsync(df[i], (const char*)hf[i] + (size_t)b0 * per, (size_t)nb * per, hipMemcpyHostToDevice,
                             s.st));
     }
-    rc = cloudsc_gpu_run(p->device, s.st, p->precision, variant, ncols, p->nproma, p->klev, &s.dev, s.scratch);
+    rc = gpu_run_impl(p->device, s.st, p->precision, variant, ncols, p->nproma, p->klev, &s.dev, s.scratch, nullptr,
+                      &p->params);
     if (rc) break;
     for (int i = 0; i < kNumFields; i++) {
       const FieldDesc& d = kFieldTable[i];
@@ -185,6 +190,15 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
   HIPCHK(hipEventRecord(p->ev1, nullptr));
   HIPCHK(hipEventSynchronize(p->ev1));
   if (rc) return rc;
+  // KSEG: a timed-out segment hand-off in any chunk invalidates the step (the
+  // error word of a slot's workspace accumulates over its chunks)
+  // (every slot's word is read and cleared, also after the first failure)
+  if (variant == CLOUDSC_VARIANT_KSEG)
+    for (auto& s : p->slots) {
+      const int r = kseg_check(p->device, s.st, s.scratch);
+      if (r && !rc) rc = r;
+    }
+  if (rc) return rc;
   float t = 0.f;
   HIPCHK(hipEventElapsedTime(&t, p->ev0, p->ev1));
   if (ms) *ms = t;
@@ -198,6 +212,7 @@ int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p) {
     if (s.st) { (void)hipStreamSynchronize(s.st); (void)hipStreamDestroy(s.st); }
   for (void* q : p->allocs) (void)hipFree(q);
   for (void* h : p->pinned) (void)hipHostUnregister(h);
+  param_set_free(&p->params);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   delete p;

@@ -75,6 +75,7 @@ struct cloudsc_gpu_state {
   void* plude_pristine;
   void* scratch;                  // SCC temporaries
   void* kseg_ws;                  // KSEG counter, flags and carried state
+  ParamSet params;                // the state's own parameter set (never shared)
   std::vector<void*> allocs;
 };
 
@@ -142,7 +143,7 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
                          long long col_offset, const cloudsc_template_t* t, const cloudsc_params_t* params) {
   if (!out || !t || !params || col_offset < 0) return CLOUDSC_EINVAL;
   *out = nullptr;
-  int rc = cloudsc_gpu_init(device, params);
+  int rc = check_params(params);
   if (rc) return rc;
   rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KSEG, ngptot, nproma, t->klev);
   if (rc) return rc;
@@ -164,6 +165,7 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
   std::memset(&s->f, 0, sizeof(s->f));
   auto fail = [&](int r) { cloudsc_state_destroy(s); return r; };
   if (hipSetDevice(device) != hipSuccess) return fail(CLOUDSC_ENODEV);
+  if ((rc = param_set_upload(&s->params, device, params))) return fail(rc);
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
   if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) return fail(CLOUDSC_EHIP);
 
@@ -249,7 +251,7 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     // result to f.plude, so repeated steps see the same input with no restore copy
     HIPCHK(hipEventRecord(ev[2 * r], s->stream));
     rc = gpu_run_impl(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f, scratch,
-                      s->plude_pristine);
+                      s->plude_pristine, &s->params);
     HIPCHK(hipEventRecord(ev[2 * r + 1], s->stream));
   }
   hipError_t e = hipStreamSynchronize(s->stream);
@@ -263,15 +265,10 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
   for (auto& x : ev) (void)hipEventDestroy(x);
   if (rc == CLOUDSC_OK && variant == CLOUDSC_VARIANT_KSEG) {
     // a segment whose predecessor never arrived gives up after a bounded spin
-    // and counts itself here: its results are invalid
-    unsigned err = 0;
-    HIPCHK(hipMemcpy(&err, (unsigned*)scratch + 1, sizeof(err), hipMemcpyDeviceToHost));
-    if (err) {
-      char msg[96];
-      std::snprintf(msg, sizeof(msg), "KSEG: %u segment hand-offs timed out", err);
-      set_error_text(msg);
-      rc = CLOUDSC_EHIP;
-    }
+    // and counts itself: its results are invalid.  The counter is re-zeroed by
+    // every launch, and a timed-out hand-off leaves the wrong carried state in
+    // every later step too, so the last step's count is the one to read.
+    rc = kseg_check(s->device, s->stream, scratch);
   }
   return rc;
 }
@@ -352,6 +349,7 @@ int cloudsc_state_destroy(cloudsc_gpu_state_t* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   for (void* p : s->allocs) (void)hipFree(p);
+  param_set_free(&s->params);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->stream) (void)hipStreamDestroy(s->stream);

@@ -14,7 +14,7 @@
  *     device against the KLON-column reference with the g % klon map, so no
  *     NGPTOT-sized host arrays exist;
  *   - HDF5 files are opened read-only (load_state.c:60,499,746 open RDWR);
- *     without input.h5 the raw dataset (tests/golden/cloudsc100) is read;
+ *     without input.h5 the raw dataset (data/cloudsc100) is read;
  *   - validation uses fabs like the Fortran ERROR_PRINT (validate_mod.F90:
  *     263-296), not the C validator's integer abs (cloudsc_validate.c:74);
  *   - the TOTAL line's col/s is NGPTOT/time (cloudsc_driver.c:261 prints the
@@ -24,12 +24,16 @@
  *     fp64 kernels reproduce the reference kernel bit for bit; fp32 is
  *     reported without a gate unless --tol is given);
  *   - --gpus N shards the columns over N devices (block-aligned contiguous
- *     ranges of the GLOBAL column index, one host thread + stream per device,
+ *     ranges of the GLOBAL column index, one host thread + stream per shard,
  *     no collective); statistics are combined on the host like the
- *     MPI_Reduce of validate_mod.F90:53-55.
+ *     MPI_Reduce of validate_mod.F90:53-55.  With fewer visible devices than
+ *     shards, shard d runs on device d % ndev (the shards of one device then
+ *     share it; results are the same bits, only the timing differs).
  *
- * nthreads is accepted and printed as NUMOMP for compatibility; the host
- * threads are one per device.
+ * nthreads is the host thread count of --variant cpu (the library's CPU
+ * variant, BASELINE.json config 1: `1 16384 32`); for the GPU variants it is
+ * accepted and printed as NUMOMP for compatibility, the host threads being
+ * one per shard.
  */
 #define _GNU_SOURCE
 #include <float.h>
@@ -46,6 +50,7 @@
 #include "cloudsc_io.h"
 
 #define ZHPM 12482329.0   /* HPM flop count for 100 columns (cloudsc_driver.c:101) */
+#define VARIANT_CPU 0     /* --variant cpu: cloudsc_cpu_run on the host cores (config 1) */
 
 typedef struct {
   int numomp, ngptot, nproma, ngpus, precision, variant, reps, warmup;
@@ -64,6 +69,7 @@ typedef struct {
   pthread_barrier_t *barrier;
   /* results */
   int rc;
+  char err[256];                  /* this shard's cloudsc_last_hip_error() (thread-local in the library) */
   double t_start, t_end;          /* seconds, CLOCK_MONOTONIC */
   float *kernel_ms;
   cloudsc_stats_t stats[CLOUDSC_NVALID];
@@ -80,13 +86,14 @@ static void usage(const char *prog) {
           "usage: %s [<nthreads> <ngptot> <nproma>] [options]\n"
           "  --gpus N              shard the columns over N devices (default 1)\n"
           "  --precision fp64|fp32 (default fp64)\n"
-          "  --variant kseg|kcache|scc (default kseg)\n"
+          "  --variant kseg|kcache|scc|cpu (default kseg; cpu = the library's CPU variant on\n"
+          "                        <nthreads> host threads, host-memory fields: BASELINE config 1)\n"
           "  --reps R              timed steps (default 1)\n"
           "  --warmup W            untimed steps before the timed ones (default 1)\n"
           "  --input FILE          input HDF5 file (default ./input.h5 when present)\n"
           "  --reference FILE      reference HDF5 file (default ./reference.h5 when present)\n"
           "  --data DIR            raw dataset directory (default $CLOUDSC_DATA or the\n"
-          "                        repository's tests/golden/cloudsc100)\n"
+          "                        repository's data/cloudsc100)\n"
           "  --tol X               relative L1 gate per field (default 10*eps = 2.2e-15 for fp64)\n"
           "  --transfer            host-buffer path: block-layout arrays in host memory,\n"
           "                        H2D -> kernel -> D2H per chunk, overlapped on streams\n"
@@ -120,6 +127,7 @@ static int parse(int argc, char **argv, options_t *o) {
       if (!strcmp(v, "kseg")) o->variant = CLOUDSC_VARIANT_KSEG;
       else if (!strcmp(v, "kcache")) o->variant = CLOUDSC_VARIANT_KCACHE;
       else if (!strcmp(v, "scc")) o->variant = CLOUDSC_VARIANT_SCC;
+      else if (!strcmp(v, "cpu")) o->variant = VARIANT_CPU;
       else { fprintf(stderr, "bad variant %s\n", v); return -1; }
     } else if (!strcmp(a, "--reps")) { NEEDV(); o->reps = atoi(v); }
     else if (!strcmp(a, "--warmup")) { NEEDV(); o->warmup = atoi(v); }
@@ -151,7 +159,7 @@ static int parse(int argc, char **argv, options_t *o) {
     if (o->numomp <= 0) o->numomp = 1;
   }
   /* KCACHE/SCC run one workgroup of NPROMA threads per block; KSEG any NPROMA */
-  const int max_nproma = o->variant == CLOUDSC_VARIANT_KSEG ? (1 << 24) : 256;
+  const int max_nproma = (o->variant == CLOUDSC_VARIANT_KSEG || o->variant == VARIANT_CPU) ? (1 << 24) : 256;
   if (o->ngptot <= 0 || o->nproma <= 0 || o->nproma > max_nproma || o->ngpus <= 0 || o->reps <= 0 ||
       o->warmup < 0) {
     fprintf(stderr, "invalid sizes: ngptot %d nproma %d (1..%d) gpus %d reps %d\n", o->ngptot, o->nproma,
@@ -161,17 +169,17 @@ static int parse(int argc, char **argv, options_t *o) {
   return 0;
 }
 
-/* the raw dataset next to the executable: <exe dir>/../tests/golden/cloudsc100 */
+/* the raw dataset next to the executable: <exe dir>/../data/cloudsc100 */
 static void default_data_dir(char *out, size_t n) {
   const char *env = getenv("CLOUDSC_DATA");
   if (env && *env) { snprintf(out, n, "%s", env); return; }
   char exe[PATH_MAX - 64];
   ssize_t len = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
-  if (len <= 0) { snprintf(out, n, "tests/golden/cloudsc100"); return; }
+  if (len <= 0) { snprintf(out, n, "data/cloudsc100"); return; }
   exe[len] = 0;
   char *slash = strrchr(exe, '/');
   if (slash) *slash = 0;
-  snprintf(out, n, "%s/../tests/golden/cloudsc100", exe);
+  snprintf(out, n, "%s/../data/cloudsc100", exe);
 }
 
 static int exists(const char *p) { return access(p, R_OK) == 0; }
@@ -195,6 +203,7 @@ static void *shard_main(void *arg) {
   s->t_end = now();
   pthread_barrier_wait(s->barrier);
   if (!s->rc && s->ref) s->rc = cloudsc_state_validate(st, s->ref, s->stats);
+  if (s->rc) snprintf(s->err, sizeof(s->err), "%s", cloudsc_last_hip_error());
   if (st) cloudsc_state_destroy(st);
   return NULL;
 }
@@ -212,7 +221,7 @@ static double print_error(const char *name, int ndim, const cloudsc_stats_t *s, 
   return rel;
 }
 
-/* ---- host-buffer path (--transfer) ---- */
+/* ---- host-memory paths: --transfer (GPU, H2D/D2H per chunk) and --variant cpu ---- */
 /* cloudsc_io input index -> cloudsc_fields_t member index */
 static int input_field_index(int i) {
   if (i < 16) return i;                 /* pt .. plu */
@@ -228,7 +237,8 @@ static const int k_out_kind[20] = {0, 0, 0, 2, 0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 
 
 static double print_error(const char *name, int ndim, const cloudsc_stats_t *s, int ngptot);
 
-static int run_transfer(const options_t *o, const cloudsc_dataset_t *ds) {
+static int run_host(const options_t *o, const cloudsc_dataset_t *ds) {
+  const int cpu = o->variant == VARIANT_CPU;
   const int es = o->precision == CLOUDSC_FP64 ? 8 : 4;
   const int nb = o->ngptot / o->nproma + (o->ngptot % o->nproma ? 1 : 0);
   const int aer = ds->params.laericesed || ds->params.laericeauto;
@@ -267,14 +277,20 @@ static int run_transfer(const options_t *o, const cloudsc_dataset_t *ds) {
   }
   const size_t plude_bytes = (size_t)nb * ds->klev * o->nproma * es;
   cloudsc_host_pipeline_t *pipe = NULL;
-  if (!rc) rc = cloudsc_gpu_init(0, &ds->params);
-  if (!rc) rc = cloudsc_host_pipeline_create(&pipe, 0, o->precision, o->ngptot, o->nproma, ds->klev,
-                                             o->chunk_blocks, o->nstreams, &f);
+  if (!rc && !cpu) rc = cloudsc_gpu_init(0, &ds->params);
+  if (!rc && !cpu) rc = cloudsc_host_pipeline_create(&pipe, 0, o->precision, o->ngptot, o->nproma, ds->klev,
+                                                     o->chunk_blocks, o->nstreams, &f);
   double total_ms = 0.0;
   for (int r = 0; r < o->warmup + o->reps && !rc; r++) {
     memcpy(f.plude, plude0, plude_bytes);                 /* INOUT restored, outside the timing */
     double ms = 0.0;
-    rc = cloudsc_host_pipeline_run(pipe, o->variant, &ms);
+    if (cpu) {
+      double secs = 0.0;
+      rc = cloudsc_cpu_run(o->numomp, o->ngptot, o->nproma, ds->klev, &ds->params, &f, &secs);
+      ms = 1e3 * secs;
+    } else {
+      rc = cloudsc_host_pipeline_run(pipe, o->variant, &ms);
+    }
     if (r >= o->warmup) total_ms += ms;
   }
   if (pipe) cloudsc_host_pipeline_destroy(pipe);
@@ -288,9 +304,14 @@ static int run_transfer(const options_t *o, const cloudsc_dataset_t *ds) {
            "tid#", "Time(msec)", "MFlops/s", "col/s");
     printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d TOTAL\n", o->numomp, o->ngptot, o->ngptot, nb, o->nproma, -1,
            (int)(t * 1000.), (int)(1.0e-06 * ZHPM * (cols / 100.) / t), (int)(cols / t));
-    printf(" TIMING: steps=%d transfer_ms_per_step=%.4f columns_per_s=%.1f host_bytes=%zu chunk_blocks=%d "
-           "streams=%d (H2D + kernel + D2H, pinned host memory)\n",
-           o->reps, total_ms / o->reps, cols / t, host_bytes, o->chunk_blocks, o->nstreams);
+    if (cpu)
+      printf(" TIMING: steps=%d cpu_ms_per_step=%.4f columns_per_s=%.1f host_bytes=%zu threads=%d "
+             "(cloudsc_cpu_run, host cores)\n",
+             o->reps, total_ms / o->reps, cols / t, host_bytes, o->numomp);
+    else
+      printf(" TIMING: steps=%d transfer_ms_per_step=%.4f columns_per_s=%.1f host_bytes=%zu chunk_blocks=%d "
+             "streams=%d (H2D + kernel + D2H, pinned host memory)\n",
+             o->reps, total_ms / o->reps, cols / t, host_bytes, o->chunk_blocks, o->nstreams);
     if (ds->has_reference) {
       printf(" %20s %s %20s %20s %20s %20s %20s\n", "Variable", "Dim", "MinValue", "MaxValue", "AbsMaxErr",
              "AvgAbsErr/GP", "MaxRelErr-%");
@@ -313,7 +334,8 @@ static int run_transfer(const options_t *o, const cloudsc_dataset_t *ds) {
         printf(" VALIDATION: reported only (fp32 vs the fp64 reference; worst relative L1 error %.3e)\n", worst);
     }
   } else {
-    fprintf(stderr, "dwarf-cloudsc-amd --transfer: %s (%s)\n", cloudsc_strerror(rc), cloudsc_last_hip_error());
+    fprintf(stderr, "dwarf-cloudsc-amd %s: %s (%s)\n", cpu ? "--variant cpu" : "--transfer", cloudsc_strerror(rc),
+            cloudsc_last_hip_error());
   }
   for (int i = 0; i < 48; i++) free(fp[i]);
   free(plude0);
@@ -360,24 +382,34 @@ int main(int argc, char **argv) {
     return rc ? EXIT_FAILURE : EXIT_SUCCESS;
   }
 
+  if (o.variant == VARIANT_CPU) {
+    if (o.precision != CLOUDSC_FP64 || o.ngpus != 1 || o.transfer) {
+      fprintf(stderr, "dwarf-cloudsc-amd: --variant cpu runs fp64 on the host (no --gpus/--transfer/fp32)\n");
+      cloudsc_io_free(&ds);
+      return EXIT_FAILURE;
+    }
+    printf(" CLOUDSC-AMD: fp64, variant cpu (cloudsc_cpu_run, %d host thread(s)); state: %s\n", o.numomp,
+           ds.source);
+    rc = run_host(&o, &ds);
+    cloudsc_io_free(&ds);
+    return rc;
+  }
+
   int ndev = 0;
   if ((rc = cloudsc_gpu_device_count(&ndev)) || ndev <= 0) {
     fprintf(stderr, "dwarf-cloudsc-amd: no HIP device (%s)\n", rc ? cloudsc_strerror(rc) : "0 devices");
     cloudsc_io_free(&ds);
     return EXIT_FAILURE;
   }
-  if (o.ngpus > ndev) {
-    fprintf(stderr, "dwarf-cloudsc-amd: --gpus %d but only %d device(s)\n", o.ngpus, ndev);
-    cloudsc_io_free(&ds);
-    return EXIT_FAILURE;
-  }
+  if (o.ngpus > ndev)
+    printf(" CLOUDSC-AMD: %d shards on %d visible device(s): shard d runs on device d %% %d\n", o.ngpus, ndev, ndev);
 
   if (o.transfer) {
     printf(" CLOUDSC-AMD: %s, variant %s, host-buffer path (--transfer), 1 device; state: %s\n",
            o.precision == CLOUDSC_FP64 ? "fp64" : "fp32",
            o.variant == CLOUDSC_VARIANT_KSEG ? "kseg" : o.variant == CLOUDSC_VARIANT_KCACHE ? "kcache" : "scc",
            ds.source);
-    rc = run_transfer(&o, &ds);
+    rc = run_host(&o, &ds);
     cloudsc_io_free(&ds);
     return rc;
   }
@@ -406,7 +438,7 @@ int main(int argc, char **argv) {
     if (col + cols > o.ngptot) cols = o.ngptot - col;
     if (cols <= 0) break;
     shard_t *s = &sh[nused++];
-    s->device = d; s->ngptot = (int)cols; s->col_offset = col; s->nproma = o.nproma;
+    s->device = d % ndev; s->ngptot = (int)cols; s->col_offset = col; s->nproma = o.nproma;
     s->precision = o.precision; s->variant = o.variant; s->reps = o.reps; s->warmup = o.warmup;
     s->tmpl = &tmpl; s->params = &ds.params; s->ref = ds.has_reference ? &ref : NULL; s->barrier = &bar;
     s->kernel_ms = (float *)calloc((size_t)o.reps, sizeof(float));
@@ -423,8 +455,8 @@ int main(int argc, char **argv) {
   int failed = 0;
   for (int d = 0; d < nused; d++)
     if (sh[d].rc) {
-      fprintf(stderr, "dwarf-cloudsc-amd: device %d: %s (%s)\n", sh[d].device, cloudsc_strerror(sh[d].rc),
-              cloudsc_last_hip_error());
+      fprintf(stderr, "dwarf-cloudsc-amd: shard %d (device %d): %s (%s)\n", d, sh[d].device,
+              cloudsc_strerror(sh[d].rc), sh[d].err);
       failed = 1;
     }
   if (failed) { cloudsc_io_free(&ds); return EXIT_FAILURE; }

@@ -3,8 +3,11 @@
  *
  * Plain C: no C++ or torch types, plain pointers and sizes.  Every entry point
  * returns 0 on success or a negative CLOUDSC_E* code; the library never calls
- * exit().  State is per device (no mutable process globals), so one host thread
- * per device -- or one thread driving N devices -- is safe.
+ * exit().  Parameters live in per-parameter-set device blocks: each device has
+ * a default set (cloudsc_gpu_init, used by cloudsc_gpu_run), and every state
+ * and host pipeline owns a private copy, so states with different parameters
+ * can be interleaved on one device.  One host thread per device -- or one
+ * thread driving N devices -- is safe.
  *
  * Which reference interface each declaration replaces (paths relative to the
  * lukasm91/dwarf-p-cloudsc checkout):
@@ -17,10 +20,13 @@
  *                         (src/cloudsc_c/cloudsc/cloudsc_c.h:18-29) and of the
  *                         CUDA kernel (src/cloudsc_cuda/cloudsc/cloudsc_c_k_caching.cu:13-40)
  *   cloudsc_gpu_init   <- cudaMemcpy of the TECLDP struct + the 28 by-value
- *                         constants (src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:383,412-416)
+ *                         constants (src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:312,383,412-416)
+ *   cloudsc_gpu_check  <- the cudaPeekAtLastError/cudaDeviceSynchronize check
+ *                         after the launch (cloudsc_driver.cu:419-420)
+ *   cloudsc_cpu_run    <- the CPU dwarf's OpenMP block loop calling cloudsc_c()
+ *                         (src/cloudsc_c/cloudsc/cloudsc_driver.c:183-217, kernel
+ *                         cloudsc_c.c:19-2587, declared cloudsc_c.h:18-29)
  *   cloudsc_gpu_run    <- cloudsc_c<<<grid,nproma>>>(...) (cloudsc_driver.cu:391-416)
- *                         and, for the CPU dwarf, the OpenMP block loop calling
- *                         cloudsc_c() (src/cloudsc_c/cloudsc/cloudsc_driver.c:183-217)
  *   cloudsc_gpu_state_* <- the driver plumbing around the kernel: load+expand
  *                         (load_state.c:69-184,279), timing (cloudsc_driver.c:181-262),
  *                         validation (src/common/module/validate_mod.F90:118-296)
@@ -49,8 +55,6 @@ extern "C" {
 #endif
 
 #define CLOUDSC_NCLV 5          /* ql, qi, qr, qs, qv (yoecldp_c.h:13-18)            */
-#define CLOUDSC_MAX_KLEV 256    /* kernels keep the column in registers: no klev cap  */
-                                /* other than the carried-state size; checked on entry */
 
 /* precision selector */
 #define CLOUDSC_FP64 8
@@ -70,6 +74,7 @@ extern "C" {
 #define CLOUDSC_ENOINIT     (-4)   /* cloudsc_gpu_init not called for this device           */
 #define CLOUDSC_ENOMEM      (-5)   /* device or host allocation failed                        */
 #define CLOUDSC_EIO         (-6)   /* file could not be read / wrong format                   */
+#define CLOUDSC_EHANDOFF    (-7)   /* a KSEG segment hand-off timed out: outputs invalid      */
 
 /* ------------------------------------------------------------------------ */
 /* Parameters: YOMCST + YOETHF + TECLDP (without rbeta/rbetap1) + PTSPHY     */
@@ -131,8 +136,12 @@ typedef struct cloudsc_fields {
 /* Number of visible HIP devices. */
 int cloudsc_gpu_device_count(int *count);
 
-/* Copy the parameter block into the device's __constant__ mirrors (fp64 and
- * fp32).  Must be called once per device before cloudsc_gpu_run. */
+/* Set the device's default parameter set (fp64 and fp32 mirrors, folded on
+ * the host) used by cloudsc_gpu_run.  Must be called once per device before
+ * cloudsc_gpu_run.  Calling it again replaces the set in place: it first waits
+ * for all work on the device (hipDeviceSynchronize), so launches already
+ * queued keep the parameters they were launched with.  States and host
+ * pipelines are not affected (they hold their own copy). */
 int cloudsc_gpu_init(int device, const cloudsc_params_t *params);
 
 /* Enqueue one CLOUDSC step over ngptot columns on `stream` (a hipStream_t, or
@@ -152,13 +161,56 @@ int cloudsc_gpu_run(int device, void *stream, int precision, int variant,
 /* Bytes of device scratch a variant needs for (ngptot, nproma, klev, precision); 0 for KCACHE. */
 long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev);
 
+/* Wait for `stream` and report failures the kernels count on the device.
+ * For KSEG: a segment whose predecessor did not hand over its carried state
+ * within the spin bound gives up and counts itself in the workspace; its
+ * columns are then wrong.  The count accumulates over the KSEG launches on
+ * `scratch` until this call reads it (and clears it): CLOUDSC_EHANDOFF if it is
+ * non-zero.  Callers of cloudsc_gpu_run with KSEG should call it after their
+ * launches (the state and pipeline APIs do).  Other variants: only the sync. */
+int cloudsc_gpu_check(int device, void *stream, int variant, void *scratch);
+
+/* Diagnostic: the number of polls a KSEG consumer makes before it gives up
+ * (default 2^24, restored by a negative value).  0 makes every hand-off fail
+ * without polling -- used by the tests of the error path. */
+int cloudsc_debug_set_kseg_spin_limit(long long limit);
+
+/* Diagnostic: override the KSEG schedule for this process -- nseg level
+ * segments per column (1..16) and a grid of `grid` workgroups -- 0 restores
+ * the measured default (2 guided segments, one workgroup per resident slot).
+ * The result bits do not depend on either; the tests use it to exercise the
+ * hand-offs with few workgroups and many segments. */
+int cloudsc_debug_set_kseg_schedule(int nseg, int grid);
+
 /* Human-readable message for an error code; last HIP error string of this thread. */
 const char *cloudsc_strerror(int code);
 const char *cloudsc_last_hip_error(void);
 
+/* Measurement: the achievable HBM bandwidth of this device, a STREAM copy of
+ * `bytes` (>= 1 MiB) into a second buffer (2 x bytes moved per launch), best
+ * of `reps` launches after one warm-up, in GB/s (10^9 B/s).  bench.py reports
+ * it as roofline.achievable_peak beside the 8 TB/s spec. */
+int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, double *gbps);
+
 /* ABI introspection for bindings: sizeof of the public structs
  * (0 params, 1 fields, 2 template, 3 reference, 4 stats), -1 otherwise. */
 long long cloudsc_abi_sizeof(int which);
+
+/* ------------------------------------------------------------------------ */
+/* CPU variant (BASELINE.json config 1): explicitly selected, never a fallback */
+/* ------------------------------------------------------------------------ */
+
+/* One CLOUDSC step over ngptot columns in HOST memory (block layout, fp64),
+ * on `nthreads` host threads (<= 0: all hardware threads) taking NPROMA blocks
+ * from a shared counter -- the C dwarf's OpenMP block loop
+ * (src/cloudsc_c/cloudsc/cloudsc_driver.c:183-217) around the kernel
+ * cloudsc_c() (cloudsc_c.c:19-2587).  The per-level physics is the same source
+ * the GPU kernels are built from, compiled for the host; the output is the
+ * reference kernel's bit for bit.  Same output contract as cloudsc_gpu_run
+ * (every output element written, plude read-modify-write).  *seconds (may be
+ * NULL) = wall time of the block loop.  Needs no GPU. */
+int cloudsc_cpu_run(int nthreads, int ngptot, int nproma, int klev, const cloudsc_params_t *params,
+                    const cloudsc_fields_t *host_fields, double *seconds);
 
 /* ------------------------------------------------------------------------ */
 /* Dwarf plumbing on the device: expand a KLON-column template to NGPTOT      */
@@ -213,7 +265,8 @@ int cloudsc_state_create(cloudsc_gpu_state_t **state, int device, int precision,
                          const cloudsc_template_t *tmpl, const cloudsc_params_t *params);
 
 /* Device pointers of the state's buffers (block layout) -- for callers that
- * want to drive cloudsc_gpu_run themselves. */
+ * want to drive cloudsc_gpu_run themselves (cloudsc_gpu_run uses the device's
+ * default parameter set, not the state's). */
 int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out);
 
 /* Restore plude from the pristine copy -- for callers that run in place
@@ -221,11 +274,13 @@ int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out
 int cloudsc_state_reset(cloudsc_gpu_state_t *state);
 
 /* Launch `reps` back-to-back steps of `variant` on the state's stream and
- * time each with HIP events recorded on that stream.  The INOUT field plude
+ * time each with HIP events recorded on that stream, with the state's own
+ * parameter set.  The INOUT field plude
  * is taken out of place: every step reads the pristine input copy and writes
  * its result to the state's plude buffer, so repeated steps compute the same
  * step without a restore copy.  ms_per_step[reps] receives the per-step
- * kernel time (may be NULL). */
+ * kernel time (may be NULL).  KSEG: CLOUDSC_EHANDOFF if a segment hand-off
+ * timed out (cloudsc_gpu_check). */
 int cloudsc_state_run(cloudsc_gpu_state_t *state, int variant, int reps, float *ms_per_step);
 
 /* Wait for all work of the state's stream. */
@@ -255,14 +310,16 @@ typedef struct cloudsc_host_pipeline cloudsc_host_pipeline_t;
  * precision's element type, ktype int).  The arrays are pinned in place
  * (hipHostRegister) until destroy; device buffers for `nstreams` chunks of
  * `chunk_blocks` blocks are allocated here.  cloudsc_gpu_init must have been
- * called for the device. */
+ * called for the device; the pipeline keeps a copy of the device's default
+ * parameter set as it is at creation. */
 int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t **pipe, int device, int precision, int ngptot,
                                  int nproma, int klev, int chunk_blocks, int nstreams,
                                  const cloudsc_fields_t *host);
 
 /* One step over all columns: per chunk H2D(inputs, plude) -> kernel -> D2H
  * (outputs, plude) on stream chunk % nstreams.  *ms = elapsed time of the
- * whole pipeline (transfers included), HIP events on the null stream. */
+ * whole pipeline (transfers included), HIP events on the null stream.
+ * KSEG: CLOUDSC_EHANDOFF if a segment hand-off timed out in any chunk. */
 int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t *pipe, int variant, double *ms);
 
 int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t *pipe);

@@ -72,6 +72,13 @@ def run_oracle(ds: "ca.Dataset", ngptot: int, nproma: int, precision: int = ca.F
 def run_ref(ds: "ca.Dataset", ngptot: int, nproma: int, nthreads: int = 0, col_offset: int = 0):
     """Same for the reference kernel itself (fp64 only)."""
     st = ca.make_host_state(ds, ngptot, nproma, ca.FP64, col_offset)
+    return st, run_ref_state(ds, st, nthreads)
+
+
+def run_ref_state(ds: "ca.Dataset", st: "ca.HostState", nthreads: int = 0) -> float:
+    """The reference kernel on an already expanded host state (plude is INOUT:
+    the caller restores it between runs).  Returns seconds of the block loop."""
+    ngptot, nproma = st.ngptot, st.nproma
     p = ca.Params.from_dict(ds.params)
     f = st.fields()
     secs = C.c_double()
@@ -79,4 +86,4 @@ def run_ref(ds: "ca.Dataset", ngptot: int, nproma: int, nthreads: int = 0, col_o
                                    C.byref(secs))
     if rc != 0:
         raise RuntimeError("cloudsc_ref_run failed: %d" % rc)
-    return st, secs.value
+    return secs.value

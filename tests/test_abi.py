@@ -62,6 +62,7 @@ def test_strerror_and_scratch_sizes(lib):
     assert lib.cloudsc_strerror(0) == b"success"
     assert lib.cloudsc_strerror(-1) == b"invalid argument"
     assert lib.cloudsc_strerror(-99) == b"unknown error"
+    assert b"hand-off" in lib.cloudsc_strerror(-7)
     # KCACHE needs no workspace; SCC and KSEG do; bad sizes -> -1
     assert lib.cloudsc_gpu_scratch_bytes(ca.FP64, ca.VARIANT_KCACHE, 163840, 128, 137) == 0
     kseg = lib.cloudsc_gpu_scratch_bytes(ca.FP64, ca.VARIANT_KSEG, 163840, 128, 137)

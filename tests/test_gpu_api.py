@@ -1,0 +1,202 @@
+"""GPU tests of the boundary's contracts beyond the numerics of one run:
+
+* parameter sets are per state (and per host pipeline), so states with
+  different physics options interleave on one device without seeing each
+  other's parameters (the reference passes TECLDP by pointer per launch,
+  src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:312,383,411);
+* a timed-out KSEG segment hand-off is reported (CLOUDSC_EHANDOFF) through
+  every path: the state API, the host pipeline, and cloudsc_gpu_check after a
+  low-level cloudsc_gpu_run;
+* BASELINE.json configs 2 and 4 at their full size (163840 columns): SCC fp64
+  at NPROMA 128 bit-equal to KCACHE, and SCC-k-caching fp32 bit-equal to the
+  fp32 restatement (driver shape: src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:391-397).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import cloudsc_amd as ca
+from test_gpu_parity import bitwise_mismatches, field_report, oracle_outputs, rel_l1
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    lib = ca.gpu_lib()
+    assert ca.device_count() > 0
+    return lib
+
+
+def outputs_of(g, variant, reps=1):
+    g.run(variant, reps)
+    return g.outputs()
+
+
+def test_interleaved_states_keep_their_parameters(lib, ds, oracle_mod):
+    """Three states on device 0 -- NSSOPT 0, NSSOPT 1 (the data set's), and the
+    aerosol flags on -- created first, then run interleaved with no sync in
+    between; a cloudsc_gpu_init with yet another parameter set in the middle
+    must not touch them.  Each matches its own oracle bit for bit."""
+    import make_fixtures as mf
+    s0 = ds.copy()
+    s0.params["nssopt"] = 0
+    s1 = ds.copy()
+    s1.params["nssopt"] = 1
+    s_aer = mf.with_aerosols(ds)
+    cases = [("nssopt0", s0), ("nssopt1", s1), ("aerosol", s_aer)]
+    ngptot, nproma = 1000, 128
+    states = [(name, s, ca.GpuState(s, ngptot, nproma)) for name, s in cases]
+    try:
+        # enqueue on all three streams before anything is read back
+        for variant in (ca.VARIANT_KSEG, ca.VARIANT_KCACHE):
+            for _, _, g in states:
+                ca.check(lib.cloudsc_state_run(g.h, variant, 2, None))
+            other = ds.copy()
+            other.params["nssopt"] = 3
+            p = ca.Params.from_dict(other.params)
+            ca.check(lib.cloudsc_gpu_init(0, C.byref(p)))    # the device default set only
+        results = {name: g.outputs() for name, _, g in states}
+    finally:
+        for _, _, g in states:
+            g.close()
+    for name, s in cases:
+        ref = oracle_outputs(oracle_mod, s, ngptot, nproma)
+        assert bitwise_mismatches(results[name], ref) == {}, name
+    # the parameter sets do differ in their results
+    assert not np.array_equal(results["nssopt0"]["tendency_loc_q"], results["nssopt1"]["tendency_loc_q"])
+
+
+def test_gpu_run_uses_the_device_default_set(lib, ds, oracle_mod):
+    """cloudsc_gpu_run runs with the set of the latest cloudsc_gpu_init."""
+    s0 = ds.copy()
+    s0.params["nssopt"] = 0
+    g = ca.GpuState(ds, 512, 128)          # buffers; the state's own set is NSSOPT 1
+    try:
+        f = ca.Fields()
+        ca.check(lib.cloudsc_state_fields(g.h, C.byref(f)))
+        for s in (s0, ds):
+            p = ca.Params.from_dict(s.params)
+            ca.check(lib.cloudsc_gpu_init(0, C.byref(p)))
+            ca.check(lib.cloudsc_state_reset(g.h))
+            ca.check(lib.cloudsc_state_sync(g.h))
+            ca.check(lib.cloudsc_gpu_run(0, None, ca.FP64, ca.VARIANT_KCACHE, 512, 128, ds.klev, C.byref(f), None))
+            ca.check(lib.cloudsc_gpu_check(0, None, ca.VARIANT_KCACHE, None))
+            out = g.outputs()
+            assert bitwise_mismatches(out, oracle_outputs(oracle_mod, s, 512, 128)) == {}, s.params["nssopt"]
+    finally:
+        g.close()
+
+
+@pytest.fixture
+def forced_handoff_failure():
+    """Spin limit 0: every KSEG consumer gives up without polling; 4 segments so
+    that every column has hand-offs."""
+    ca.kseg_schedule(4, 0)
+    ca.kseg_spin_limit(0)
+    yield
+    ca.kseg_spin_limit(-1)
+    ca.kseg_schedule(0, 0)
+
+
+def test_handoff_timeout_state_api(lib, ds, forced_handoff_failure):
+    g = ca.GpuState(ds, 2000, 64)
+    try:
+        rc = lib.cloudsc_state_run(g.h, ca.VARIANT_KSEG, 1, None)
+        assert rc == ca.EHANDOFF, rc
+        assert b"hand-off" in lib.cloudsc_last_hip_error()
+        # the error was read and cleared: with the default bound the next run is clean
+        ca.kseg_spin_limit(-1)
+        ca.check(lib.cloudsc_state_run(g.h, ca.VARIANT_KSEG, 1, None))
+        a = g.outputs()
+        ca.check(lib.cloudsc_state_run(g.h, ca.VARIANT_KCACHE, 1, None))
+        b = g.outputs()
+        assert bitwise_mismatches(a, b) == {}
+    finally:
+        g.close()
+
+
+def test_handoff_timeout_low_level(lib, ds, forced_handoff_failure):
+    g = ca.GpuState(ds, 2000, 64)
+    ws = None
+    try:
+        f = ca.Fields()
+        ca.check(lib.cloudsc_state_fields(g.h, C.byref(f)))
+        p = ca.Params.from_dict(ds.params)
+        ca.check(lib.cloudsc_gpu_init(0, C.byref(p)))
+        nbytes = lib.cloudsc_gpu_scratch_bytes(ca.FP64, ca.VARIANT_KSEG, 2000, 64, ds.klev)
+        assert nbytes > 0
+        # caller-owned device workspace, from the HIP runtime the library itself uses
+        hip = C.CDLL("libamdhip64.so.7")
+        ptr = C.c_void_p()
+        assert hip.hipMalloc(C.byref(ptr), C.c_size_t(nbytes)) == 0
+        ws = (hip, ptr)
+        ca.check(lib.cloudsc_state_sync(g.h))
+        # two launches, the first fails: the count accumulates until the check
+        ca.check(lib.cloudsc_gpu_run(0, None, ca.FP64, ca.VARIANT_KSEG, 2000, 64, ds.klev, C.byref(f), ptr))
+        ca.kseg_spin_limit(-1)
+        ca.check(lib.cloudsc_gpu_run(0, None, ca.FP64, ca.VARIANT_KSEG, 2000, 64, ds.klev, C.byref(f), ptr))
+        assert lib.cloudsc_gpu_check(0, None, ca.VARIANT_KSEG, ptr) == ca.EHANDOFF
+        assert lib.cloudsc_gpu_check(0, None, ca.VARIANT_KSEG, ptr) == 0        # cleared by the read
+    finally:
+        if ws is not None:
+            ws[0].hipFree(ws[1])
+        g.close()
+
+
+def test_handoff_timeout_host_pipeline(lib, ds, forced_handoff_failure):
+    hp = ca.HostPipeline(ds, 1000, 64, chunk_blocks=4, nstreams=2)
+    try:
+        with pytest.raises(ca.CloudscError) as e:
+            hp.run(ca.VARIANT_KSEG)
+        assert e.value.code == ca.EHANDOFF
+        ca.kseg_spin_limit(-1)
+        hp.run(ca.VARIANT_KSEG)
+    finally:
+        hp.close()
+
+
+def test_bitwise_scc_full_size(lib, ds):
+    """BASELINE.json config 2: SCC fp64 (HBM temporaries), NGPTOT 163840,
+    NPROMA 128 -- all 21 fields bit-equal to KCACHE on the same state (KCACHE is
+    pinned to the oracle at this size by test_bitwise_full_size_vs_oracle)."""
+    g = ca.GpuState(ds, 163840, 128)
+    try:
+        scc = outputs_of(g, ca.VARIANT_SCC)
+        kc = outputs_of(g, ca.VARIANT_KCACHE)
+    finally:
+        g.close()
+    assert bitwise_mismatches(scc, kc) == {}
+
+
+def test_bitwise_fp32_full_size(lib, ds, oracle_mod):
+    """BASELINE.json config 4: SCC-k-caching fp32, NGPTOT 163840 (NPROMA 64, the
+    fp32 bench default) -- bit-equal to the fp32 restatement at the same size;
+    per-field relL1 vs reference.h5 (fp64) printed, and no worse than 2x the fp32
+    CPU restatement's own (SURVEY.md §8c gate; fp32 is parity-unpinned beyond the
+    restatement: the reference has no fp32 C kernel)."""
+    n = 163840
+    out = {}
+    for variant in (ca.VARIANT_KCACHE, ca.VARIANT_KSEG):
+        g = ca.GpuState(ds, n, 64, ca.FP32)
+        try:
+            out[variant] = outputs_of(g, variant)
+        finally:
+            g.close()
+    ref = oracle_outputs(oracle_mod, ds, n, 64, precision=ca.FP32)
+    for variant, o in out.items():
+        bad = {}
+        for _, k in ca.VALIDATED:
+            a = np.ascontiguousarray(o[k], dtype=np.float32).view(np.uint32)
+            r = np.ascontiguousarray(ref[k], dtype=np.float32).view(np.uint32)
+            m = int(np.count_nonzero(a != r))
+            if m:
+                bad[k] = m
+        assert bad == {}, (variant, bad)
+    gold = {k: np.take(ds.reference[k], np.arange(n) % ds.klon, axis=-1) for _, k in ca.VALIDATED}
+    g_rep = field_report(out[ca.VARIANT_KCACHE], gold)
+    c_rep = field_report(ref, gold)
+    for k in g_rep:
+        print("fp32 @163840 vs reference.h5 %-18s relL1 gpu %.3e cpu %.3e" % (k, g_rep[k][0], c_rep[k][0]))
+        assert g_rep[k][0] <= 2.0 * c_rep[k][0] + 1e-6, k

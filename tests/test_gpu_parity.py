@@ -231,21 +231,12 @@ def test_low_level_run_entry(lib, ds):
 # ---- persistent segmented k-caching (KSEG): must be bit-identical to KCACHE ----
 @pytest.fixture
 def kseg_env():
-    import os
-    saved = {k: os.environ.get(k) for k in ("CLOUDSC_KSEG_NSEG", "CLOUDSC_KSEG_GRID")}
-
-    def set_env(nseg=None, grid=None):
-        for k, v in (("CLOUDSC_KSEG_NSEG", nseg), ("CLOUDSC_KSEG_GRID", grid)):
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = str(v)
-    yield set_env
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
+    """Override the KSEG schedule (segments per column, grid) through the
+    library's diagnostic setter; restored to the defaults afterwards."""
+    def set_sched(nseg=None, grid=None):
+        ca.kseg_schedule(nseg or 0, grid or 0)
+    yield set_sched
+    ca.kseg_schedule(0, 0)
 
 
 @pytest.mark.parametrize("nseg,grid", [(1, None), (2, None), (4, None), (8, None), (4, 3), (8, 1), (3, 5)])

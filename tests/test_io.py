@@ -2,7 +2,7 @@
 dwarf-p-cloudsc_amd/csrc/cloudsc_io.c through libcloudsc_io.so, and the
 dwarf-cloudsc-amd CLI paths that need no device.
 
-Pinned against the reference's own files: tests/golden/cloudsc100 holds the
+Pinned against the reference's own files: data/cloudsc100 holds the
 Serialbox arrays of the reference's data/, tests/golden/reference.h5 is
 config-files/reference.h5.  The HDF5 writer must reproduce that file exactly
 from the raw arrays (the input.h5 regeneration tool of SURVEY.md §8f-1)."""
@@ -22,6 +22,7 @@ PKG = os.path.join(REPO, "dwarf-p-cloudsc_amd")
 IO_LIB = os.path.join(PKG, "libcloudsc_io.so")
 DWARF = os.path.join(PKG, "dwarf-cloudsc-amd")
 GOLDEN = os.path.join(REPO, "tests", "golden")
+DATA = os.path.join(REPO, "data", "cloudsc100")
 REF_H5_UPSTREAM = "/root/reference/config-files/reference.h5"
 
 NIN = 28
@@ -77,7 +78,7 @@ def arrays(d: Dataset):
     return inp, ref
 
 
-def load_raw(io, path=os.path.join(GOLDEN, "cloudsc100")):
+def load_raw(io, path=DATA):
     d = Dataset()
     rc = io.cloudsc_io_load_raw(path.encode(), 1, C.byref(d))
     assert rc == 0, io.cloudsc_io_last_error()
@@ -101,7 +102,7 @@ def test_raw_reader_matches_python_loader(io, ds):
 def test_raw_reader_errors(io, tmp_path):
     d = Dataset()
     assert io.cloudsc_io_load_raw(str(tmp_path).encode(), 1, C.byref(d)) == -6     # no manifest
-    shutil.copytree(os.path.join(GOLDEN, "cloudsc100"), tmp_path / "ds")
+    shutil.copytree(DATA, tmp_path / "ds")
     with open(tmp_path / "ds" / "input_PT.dat", "r+b") as fh:                     # truncated field
         fh.truncate(100)
     assert io.cloudsc_io_load_raw(str(tmp_path / "ds").encode(), 1, C.byref(d)) == -6

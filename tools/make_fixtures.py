@@ -2,7 +2,7 @@
 """Generate the committed golden fixtures under tests/golden/ (run in the build
 container, where /root/reference exists; the GPU box only reads the result).
 
-1. tests/golden/cloudsc100/  -- the reference's own 100-column data set:
+1. data/cloudsc100/  -- the reference's own 100-column data set:
    * input_<FIELD>.dat     raw little-endian arrays copied byte-for-byte from
                            data/input_<FIELD>.dat (Serialbox binary; C order
                            [lev][klon] / [nclv][lev][klon] / [klon], i.e. the
@@ -50,7 +50,7 @@ def json_params(meta_path):
 
 
 def make_cloudsc100():
-    d = os.path.join(OUT, "cloudsc100")
+    d = os.path.join(REPO, "data", "cloudsc100")
     os.makedirs(d, exist_ok=True)
     params, klon, klev = json_params(os.path.join(REFDATA, "MetaData-input.json"))
     ca.write_params_txt(os.path.join(d, "params.txt"), params)
@@ -139,7 +139,7 @@ def make_scenarios():
     import oracle  # the compiled reference kernel (oracle/_ref)
     if not oracle.ref_available():
         raise SystemExit("oracle/_ref/libcloudsc_ref.so missing: make -C oracle")
-    ds = ca.load_dataset(os.path.join(OUT, "cloudsc100"))
+    ds = ca.load_dataset(os.path.join(REPO, "data", "cloudsc100"))
     for name in ("W", "M"):
         s = scenario(ds, name)
         st, _ = oracle.run_ref(s, s.klon, s.klon, nthreads=1)
@@ -157,7 +157,7 @@ def make_scenarios():
 
 def load_scenario(name, base=None):
     """Dataset with the scenario's perturbed inputs and reference outputs."""
-    base = base or ca.load_dataset(os.path.join(OUT, "cloudsc100"))
+    base = base or ca.load_dataset(os.path.join(REPO, "data", "cloudsc100"))
     z = np.load(os.path.join(OUT, "scenario_%s.npz" % name))
     s = base.copy()
     for k in z.files:

@@ -33,9 +33,12 @@ def main():
         sys.exit("no dispatches matched %r" % regex)
     fetch = sum(fe) / len(fe) * 1024.0
     write = sum(wr) / len(wr) * 1024.0
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dwarf-p-cloudsc_amd"))
+    import cloudsc_amd as ca
     entry = {"fetch_size_bytes_raw": fetch, "write_size_bytes": write,
              "hbm_bytes_per_launch": 2.0 * fetch + write, "dispatches": [len(fe), len(wr)],
-             "correction": "FETCH_SIZE x2 (gfx950 coalesced-read under-count), WRITE_SIZE as reported"}
+             "correction": "FETCH_SIZE x2 (gfx950 coalesced-read under-count), WRITE_SIZE as reported",
+             "kernel_source_hash": ca.kernel_source_hash()}
     data = json.load(open(out)) if os.path.exists(out) else {}
     data[key] = entry
     json.dump(data, open(out, "w"), indent=1, sort_keys=True)
