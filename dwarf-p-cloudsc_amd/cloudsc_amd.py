@@ -187,12 +187,36 @@ class Dataset:
                        {k: v.copy() for k, v in self.reference.items()})
 
 
+def read_serialbox_params(path: str) -> Dict[str, float]:
+    """The parameter block from a Serialbox store's MetaData-input.json
+    (global_meta_info, the input.h5 scalar names: RG, ..., YRECLDP_<NAME>;
+    logicals as 0/1), keyed like params.txt (lower case, no YRECLDP_ prefix)."""
+    g = json.load(open(os.path.join(path, "MetaData-input.json")))["global_meta_info"]
+    by_key = {}
+    for name, v in g.items():
+        key = (name[8:] if name.startswith("YRECLDP_") else name).lower()
+        by_key[key] = v["value"]
+    out: Dict[str, float] = {}
+    for n in PARAM_DOUBLES:
+        out[n] = float(by_key[n])
+    for n in PARAM_INTS:
+        out[n] = int(by_key[n])
+    return out
+
+
 def load_dataset(path: str = DATA_DIR, with_reference: bool = True) -> Dataset:
-    """Read a raw dataset directory (``input_<NAME>.dat``, ``reference_<NAME>.dat``,
-    ``params.txt``, ``manifest.json``) as written by tools/make_fixtures.py."""
-    man = json.load(open(os.path.join(path, "manifest.json")))
-    klon, klev = man["klon"], man["klev"]
-    params = read_params_txt(os.path.join(path, "params.txt"))
+    """Read a data directory: a Serialbox store (the reference's data/:
+    MetaData-input.json + input_<NAME>.dat, reference_<NAME>.dat) or the raw
+    form written by tools/make_fixtures.py (manifest.json + params.txt + the
+    same .dat arrays)."""
+    if os.path.exists(os.path.join(path, "MetaData-input.json")):
+        g = json.load(open(os.path.join(path, "MetaData-input.json")))["global_meta_info"]
+        klon, klev = int(g["KLON"]["value"]), int(g["KLEV"]["value"])
+        params = read_serialbox_params(path)
+    else:
+        man = json.load(open(os.path.join(path, "manifest.json")))
+        klon, klev = man["klon"], man["klev"]
+        params = read_params_txt(os.path.join(path, "params.txt"))
     inputs = {}
     for name, kind in {**INPUT_FIELDS, **AEROSOL_FIELDS, **INOUT_FIELDS}.items():
         fn = os.path.join(path, "input_%s.dat" % name.upper())

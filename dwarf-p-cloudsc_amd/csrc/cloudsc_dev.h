@@ -288,6 +288,56 @@ CLOUDSC_HD float cl_div(float n, float d) {
   return __builtin_fmaf(rem, r, q);
 #endif
 }
+// A divisor together with its refined reciprocal, for divisions that share a
+// divisor: cl_div(n, cl_recip(d)) runs exactly the steps of cl_div(n, d) with
+// the same reciprocal r, so the quotient is bit-identical -- the reciprocal
+// (v_rcp + its Newton steps) is computed once instead of once per division.
+template <typename real>
+struct Recip {
+  real d, r;
+};
+CLOUDSC_HD Recip<double> cl_recip(double d) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return {d, 0.0};      // host: the divisions below use d itself
+#else
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  return {d, r};
+#endif
+}
+CLOUDSC_HD Recip<float> cl_recip(float d) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return {d, 0.0f};
+#else
+  float r = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, r, 1.0f);
+  r = __builtin_fmaf(e, r, r);
+  return {d, r};
+#endif
+}
+CLOUDSC_HD double cl_div(double n, const Recip<double>& rd) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return n / rd.d;
+#else
+  const double q = n * rd.r;
+  const double rem = __builtin_fma(-rd.d, q, n);
+  return __builtin_fma(rem, rd.r, q);
+#endif
+}
+CLOUDSC_HD float cl_div(float n, const Recip<float>& rd) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return n / rd.d;
+#else
+  float q = n * rd.r;
+  float rem = __builtin_fmaf(-rd.d, q, n);
+  q = __builtin_fmaf(rem, rd.r, q);
+  rem = __builtin_fmaf(-rd.d, q, n);
+  return __builtin_fmaf(rem, rd.r, q);
+#endif
+}
 // explicit-precision form, cl_div<real>(a, b)
 template <typename real>
 CLOUDSC_HD real cl_div(typename std::common_type<real>::type n, typename std::common_type<real>::type d) {

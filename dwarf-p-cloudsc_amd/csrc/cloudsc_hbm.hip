@@ -4,10 +4,11 @@
 // pool's boxes differ by 10+ % in this kernel, so the spec fraction alone does
 // not normalise).
 //
-// A STREAM copy b[i] = a[i] over two device buffers: 16 B per lane per access,
-// four independent loads in flight per lane before the four stores,
-// non-temporal (streaming) loads and stores, a grid of resident workgroups
-// striding over the buffer.  Bytes moved = 2 x buffer size per launch.
+// A STREAM copy b[i] = a[i] over two device buffers, 16 B per lane per access
+// and four independent loads in flight per lane before the stores, in a few
+// shapes (cached or non-temporal; a resident grid striding over the buffer, or
+// one 16 KB tile per workgroup); the figure is the best launch of any shape.
+// Bytes moved = 2 x buffer size per launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,21 +23,41 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ void __launch_bounds__(256) stream_copy_kernel(const u32x4* __restrict__ a, u32x4* __restrict__ b,
-                                                           size_t n) {
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// persistent grid-stride form: four independent 16-B loads per lane in flight
+template <bool NT>
+__global__ void __launch_bounds__(256) copy_strided(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i + 3 * stride < n; i += 4 * stride) {
-    const u32x4 v0 = __builtin_nontemporal_load(a + i);
-    const u32x4 v1 = __builtin_nontemporal_load(a + i + stride);
-    const u32x4 v2 = __builtin_nontemporal_load(a + i + 2 * stride);
-    const u32x4 v3 = __builtin_nontemporal_load(a + i + 3 * stride);
-    __builtin_nontemporal_store(v0, b + i);
-    __builtin_nontemporal_store(v1, b + i + stride);
-    __builtin_nontemporal_store(v2, b + i + 2 * stride);
-    __builtin_nontemporal_store(v3, b + i + 3 * stride);
+    const u32x4 v0 = ld<NT>(a + i), v1 = ld<NT>(a + i + stride), v2 = ld<NT>(a + i + 2 * stride),
+                v3 = ld<NT>(a + i + 3 * stride);
+    st<NT>(b + i, v0); st<NT>(b + i + stride, v1); st<NT>(b + i + 2 * stride, v2); st<NT>(b + i + 3 * stride, v3);
   }
-  for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+  for (; i < n; i += stride) st<NT>(b + i, ld<NT>(a + i));
+}
+
+// one-shot form: each lane copies 4 consecutive 16-B chunks of its workgroup's 16 KB tile
+template <bool NT>
+__global__ void __launch_bounds__(256) copy_tiles(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n) {
+  const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+  u32x4 v[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (base + q * 256 < n) v[q] = ld<NT>(a + base + q * 256);
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (base + q * 256 < n) st<NT>(b + base + q * 256, v[q]);
 }
 
 }  // namespace
@@ -52,7 +73,12 @@ extern "C" int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, doub
   if (hipMalloc(&b, nvec * sizeof(u32x4)) != hipSuccess) { (void)hipFree(a); return CLOUDSC_ENOMEM; }
   int ncu = 256;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-  const int grid = ncu * 8;                      // 8 workgroups of 4 waves per CU: 32 waves/CU
+  // the shapes tried; the achievable figure is the best of them
+  struct Shape { void (*k)(const u32x4*, u32x4*, size_t); int grid; };
+  const int tiles = (int)((nvec + 1023) / 1024);
+  const Shape shapes[] = {{copy_strided<true>, ncu * 8},  {copy_strided<false>, ncu * 8},
+                          {copy_strided<true>, ncu * 16}, {copy_tiles<true>, tiles},
+                          {copy_tiles<false>, tiles}};
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = CLOUDSC_OK;
@@ -63,9 +89,10 @@ extern "C" int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, doub
   } else if (hipMemsetAsync(a, 0x3c, nvec * sizeof(u32x4), st) != hipSuccess) {
     rc = CLOUDSC_EHIP;
   } else {
-    for (int r = -1; r < reps && rc == CLOUDSC_OK; r++) {     // r = -1: untimed warm-up
+    for (int r = -1; r < reps * (int)(sizeof(shapes) / sizeof(shapes[0])) && rc == CLOUDSC_OK; r++) {
+      const Shape& sh = shapes[(r < 0 ? 0 : r) % (int)(sizeof(shapes) / sizeof(shapes[0]))];   // r = -1: warm-up
       if (hipEventRecord(e0, st) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
-      hipLaunchKernelGGL(stream_copy_kernel, dim3(grid), dim3(256), 0, st, (const u32x4*)a, (u32x4*)b, nvec);
+      hipLaunchKernelGGL(sh.k, dim3(sh.grid), dim3(256), 0, st, (const u32x4*)a, (u32x4*)b, nvec);
       if (hipGetLastError() != hipSuccess || hipEventRecord(e1, st) != hipSuccess ||
           hipEventSynchronize(e1) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
       float ms = 0.f;

@@ -202,6 +202,238 @@ static int load_params_txt(const char *path, cloudsc_params_t *p) {
   return CLOUDSC_OK;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Serialbox store (the reference's data/ directory): MetaData-<prefix>.json  */
+/* (global_meta_info: KLON, KLEV and the parameter scalars under the same     */
+/* names as input.h5; field_map: dims and element type of every field),       */
+/* ArchiveMetaData-<prefix>.json (fields_table: byte offset of each field in  */
+/* <prefix>_<FIELD>.dat per savepoint), the .dat files raw column-major       */
+/* (Fortran) arrays -- i.e. C-order [..][lev][klon].  This is what            */
+/* serialbox2hdf5/serialbox2hdf5.py:11-33 converts into input.h5, read here    */
+/* directly (the scalars the way load_state.c:538-690 reads them from HDF5).  */
+/* ------------------------------------------------------------------------ */
+typedef struct jv {
+  int type;                         /* 0 null, 1 bool, 2 number, 3 string, 4 array, 5 object */
+  double num;
+  char *str;
+  int n;
+  struct jv *items;                 /* array elements / object values */
+  char **keys;                      /* object keys */
+} jv;
+
+static void jv_free(jv *v) {
+  if (!v) return;
+  free(v->str);
+  for (int i = 0; i < v->n; i++) {
+    jv_free(&v->items[i]);
+    if (v->keys) free(v->keys[i]);
+  }
+  free(v->items);
+  free(v->keys);
+  memset(v, 0, sizeof(*v));
+}
+
+typedef struct { const char *p, *end; int err; } jparser;
+
+static void jws(jparser *j) {
+  while (j->p < j->end && (*j->p == ' ' || *j->p == '\n' || *j->p == '\r' || *j->p == '\t')) j->p++;
+}
+static char *jstring(jparser *j) {
+  if (j->p >= j->end || *j->p != '"') { j->err = 1; return NULL; }
+  j->p++;
+  size_t cap = 16, n = 0;
+  char *out = (char *)malloc(cap);
+  while (out && j->p < j->end && *j->p != '"') {
+    char c = *j->p++;
+    if (c == '\\' && j->p < j->end) {
+      c = *j->p++;
+      if (c == 'n') c = '\n'; else if (c == 't') c = '\t'; else if (c == 'u') { j->p += 4; c = '?'; }
+    }
+    if (n + 2 > cap) { cap *= 2; char *t = (char *)realloc(out, cap); if (!t) { free(out); out = NULL; break; } out = t; }
+    out[n++] = c;
+  }
+  if (!out || j->p >= j->end) { free(out); j->err = 1; return NULL; }
+  j->p++;
+  out[n] = 0;
+  return out;
+}
+static int jvalue(jparser *j, jv *v, int depth) {
+  memset(v, 0, sizeof(*v));
+  jws(j);
+  if (j->p >= j->end || depth > 64) return j->err = 1;
+  const char c = *j->p;
+  if (c == '{' || c == '[') {
+    const int obj = c == '{';
+    v->type = obj ? 5 : 4;
+    j->p++;
+    int cap = 0;
+    for (;;) {
+      jws(j);
+      if (j->p < j->end && *j->p == (obj ? '}' : ']')) { j->p++; return 0; }
+      if (v->n == cap) {
+        cap = cap ? 2 * cap : 8;
+        jv *ni = (jv *)realloc(v->items, sizeof(jv) * cap);
+        if (!ni) return j->err = 1;
+        v->items = ni;
+        if (obj) {
+          char **nk = (char **)realloc(v->keys, sizeof(char *) * cap);
+          if (!nk) return j->err = 1;
+          v->keys = nk;
+        }
+      }
+      if (obj) {
+        v->keys[v->n] = NULL;
+        memset(&v->items[v->n], 0, sizeof(jv));
+        char *k = jstring(j);
+        if (!k) return j->err = 1;
+        v->keys[v->n] = k;
+        jws(j);
+        if (j->p >= j->end || *j->p != ':') { v->n++; return j->err = 1; }
+        j->p++;
+      }
+      const int r = jvalue(j, &v->items[v->n], depth + 1);
+      v->n++;
+      if (r) return j->err = 1;
+      jws(j);
+      if (j->p < j->end && *j->p == ',') { j->p++; continue; }
+      if (j->p < j->end && *j->p == (obj ? '}' : ']')) { j->p++; return 0; }
+      return j->err = 1;
+    }
+  }
+  if (c == '"') { v->type = 3; v->str = jstring(j); return v->str ? 0 : (j->err = 1); }
+  if (!strncmp(j->p, "true", 4)) { v->type = 1; v->num = 1; j->p += 4; return 0; }
+  if (!strncmp(j->p, "false", 5)) { v->type = 1; v->num = 0; j->p += 5; return 0; }
+  if (!strncmp(j->p, "null", 4)) { v->type = 0; j->p += 4; return 0; }
+  char *e = NULL;
+  v->num = strtod(j->p, &e);     /* decimal -> double, correctly rounded by the C library */
+  if (e == j->p) return j->err = 1;
+  v->type = 2;
+  j->p = e;
+  return 0;
+}
+static const jv *jget(const jv *o, const char *key) {
+  if (!o || o->type != 5) return NULL;
+  for (int i = 0; i < o->n; i++)
+    if (!strcmp(o->keys[i], key)) return &o->items[i];
+  return NULL;
+}
+static int jparse_file(const char *path, jv *root) {
+  memset(root, 0, sizeof(*root));
+  FILE *f = fopen(path, "rb");
+  if (!f) { set_err("cannot open %s", path); return CLOUDSC_EIO; }
+  fseek(f, 0, SEEK_END);
+  long sz = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  char *text = sz > 0 ? (char *)malloc((size_t)sz) : NULL;
+  if (!text || fread(text, 1, (size_t)sz, f) != (size_t)sz) {
+    free(text); fclose(f); set_err("cannot read %s", path); return CLOUDSC_EIO;
+  }
+  fclose(f);
+  jparser j = {text, text + sz, 0};
+  jvalue(&j, root, 0);
+  free(text);
+  if (j.err || root->type != 5) { jv_free(root); set_err("%s: not a JSON object", path); return CLOUDSC_EIO; }
+  return CLOUDSC_OK;
+}
+
+/* one Serialbox field: checks dims / element type, reads it at its archive offset */
+static void *sb_read_field(const char *dir, const char *prefix, const jv *meta, const jv *archive,
+                           const char *name, long long expect, int want_int, int *rc) {
+  const jv *fm = jget(jget(meta, "field_map"), name);
+  if (!fm) { *rc = CLOUDSC_EIO; set_err("Serialbox %s: no field %s", prefix, name); return NULL; }
+  const jv *dims = jget(fm, "dims");
+  long long ne = 1;
+  for (int i = 0; dims && dims->type == 4 && i < dims->n; i++) ne *= (long long)dims->items[i].num;
+  const jv *mi = jget(fm, "meta_info");
+  const jv *et = jget(jget(mi, "__elementtype"), "value");
+  const jv *bpe = jget(jget(mi, "__bytesperelement"), "value");
+  const int esz = bpe ? (int)bpe->num : 0;
+  const int is_int = et && et->str && !strcmp(et->str, "int");
+  const int is_dbl = et && et->str && !strcmp(et->str, "double");
+  if (ne != expect || (want_int ? !(is_int && esz == 4) : !(is_dbl && esz == 8))) {
+    *rc = CLOUDSC_EIO;
+    set_err("Serialbox %s: field %s has %lld elements of %s/%d B, expected %lld of %s", prefix, name, ne,
+            et && et->str ? et->str : "?", esz, expect, want_int ? "int32" : "double");
+    return NULL;
+  }
+  long long offset = 0;
+  const jv *ft = jget(jget(archive, "fields_table"), name);   /* [[offset, checksum], ...] per savepoint */
+  if (ft && ft->type == 4 && ft->n > 0 && ft->items[0].type == 4 && ft->items[0].n > 0)
+    offset = (long long)ft->items[0].items[0].num;
+  char path[1024];
+  snprintf(path, sizeof(path), "%s/%s_%s.dat", dir, prefix, name);
+  FILE *f = fopen(path, "rb");
+  if (!f) { *rc = CLOUDSC_EIO; set_err("cannot open %s", path); return NULL; }
+  const size_t bytes = (size_t)ne * (size_t)esz;
+  void *buf = malloc(bytes ? bytes : 1);
+  if (!buf || fseek(f, (long)offset, SEEK_SET) != 0 || fread(buf, 1, bytes, f) != bytes) {
+    free(buf); fclose(f); *rc = buf ? CLOUDSC_EIO : CLOUDSC_ENOMEM; set_err("short read on %s", path); return NULL;
+  }
+  fclose(f);
+  *rc = CLOUDSC_OK;
+  return buf;
+}
+
+int cloudsc_io_load_serialbox(const char *dir, int with_reference, cloudsc_dataset_t *ds) {
+  if (!dir || !ds) return CLOUDSC_EINVAL;
+  if (!check_layout()) { set_err("cloudsc_params_t layout mismatch"); return CLOUDSC_EINVAL; }
+  memset(ds, 0, sizeof(*ds));
+  char path[1024];
+  jv meta, arch;
+  int rc;
+  snprintf(path, sizeof(path), "%s/MetaData-input.json", dir);
+  if ((rc = jparse_file(path, &meta))) return rc;
+  snprintf(path, sizeof(path), "%s/ArchiveMetaData-input.json", dir);
+  if ((rc = jparse_file(path, &arch))) { jv_free(&meta); return rc; }
+  const jv *g = jget(&meta, "global_meta_info");
+  const jv *klon = jget(jget(g, "KLON"), "value"), *klev = jget(jget(g, "KLEV"), "value");
+  rc = CLOUDSC_OK;
+  if (!klon || !klev || klon->num <= 0 || klev->num < 2) { set_err("%s: no KLON/KLEV", dir); rc = CLOUDSC_EIO; }
+  if (!rc) { ds->klon = (int)klon->num; ds->klev = (int)klev->num; }
+  /* parameters: the input.h5 scalar names (logicals -> 0/1, like hdf5_file_mod.F90:171-175) */
+  for (int i = 0; i < N_PDOUBLE && !rc; i++) {
+    const jv *v = jget(jget(g, k_param_double_names[i]), "value");
+    if (!v || (v->type != 2 && v->type != 1)) { set_err("%s: missing scalar %s", dir, k_param_double_names[i]); rc = CLOUDSC_EIO; }
+    else param_doubles(&ds->params)[i] = v->num;
+  }
+  for (int i = 0; i < N_PINT && !rc; i++) {
+    const jv *v = jget(jget(g, k_param_int_names[i]), "value");
+    if (!v || (v->type != 2 && v->type != 1)) { set_err("%s: missing scalar %s", dir, k_param_int_names[i]); rc = CLOUDSC_EIO; }
+    else param_ints(&ds->params)[i] = (int)v->num;
+  }
+  for (int i = 0; i < CLOUDSC_IO_NIN && !rc; i++) {
+    const char *name = cloudsc_io_input_names[i];
+    if (i >= CLOUDSC_IO_FIRST_AEROSOL) {          /* aerosol inputs are optional (read only under LAER*) */
+      snprintf(path, sizeof(path), "%s/input_%s.dat", dir, name);
+      if (!jget(jget(&meta, "field_map"), name) || !file_exists(path)) continue;
+    }
+    const long long ne = cloudsc_io_elems(cloudsc_io_input_kind[i], ds->klev, ds->klon);
+    void *buf = sb_read_field(dir, "input", &meta, &arch, name, ne, i == CLOUDSC_IO_KTYPE, &rc);
+    if (i == CLOUDSC_IO_KTYPE) ds->ktype = (int *)buf;
+    else ds->in[i] = (double *)buf;
+  }
+  jv_free(&meta);
+  jv_free(&arch);
+  if (!rc && with_reference) {
+    snprintf(path, sizeof(path), "%s/MetaData-reference.json", dir);
+    if (!(rc = jparse_file(path, &meta))) {
+      snprintf(path, sizeof(path), "%s/ArchiveMetaData-reference.json", dir);
+      if (!(rc = jparse_file(path, &arch))) {
+        for (int i = 0; i < CLOUDSC_NVALID && !rc; i++) {
+          const long long ne = cloudsc_io_elems(cloudsc_io_ref_kind[i], ds->klev, ds->klon);
+          ds->ref[i] = (double *)sb_read_field(dir, "reference", &meta, &arch, cloudsc_io_ref_names[i], ne, 0, &rc);
+        }
+        jv_free(&arch);
+      }
+      jv_free(&meta);
+    }
+    if (!rc) ds->has_reference = 1;
+  }
+  if (rc) { cloudsc_io_free(ds); return rc; }
+  snprintf(ds->source, sizeof(ds->source), "Serialbox store %s", dir);
+  return CLOUDSC_OK;
+}
+
 int cloudsc_io_load_raw(const char *dir, int with_reference, cloudsc_dataset_t *ds) {
   if (!dir || !ds) return CLOUDSC_EINVAL;
   if (!check_layout()) { set_err("cloudsc_params_t layout mismatch"); return CLOUDSC_EINVAL; }
@@ -551,4 +783,12 @@ void cloudsc_io_field_stats(const double *ref, int kind, int klev, int klon, con
       }
   }
   st->minval = mn; st->maxval = mx; st->maxerr = me; st->errsum = es; st->refsum = rs;
+}
+
+int cloudsc_io_load_dir(const char *dir, int with_reference, cloudsc_dataset_t *ds) {
+  if (!dir || !ds) return CLOUDSC_EINVAL;
+  char path[1024];
+  snprintf(path, sizeof(path), "%s/MetaData-input.json", dir);
+  return file_exists(path) ? cloudsc_io_load_serialbox(dir, with_reference, ds)
+                           : cloudsc_io_load_raw(dir, with_reference, ds);
 }

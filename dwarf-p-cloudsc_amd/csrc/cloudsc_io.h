@@ -60,6 +60,16 @@ long long cloudsc_io_elems(int kind, int klev, int klon);
 /* Load from a raw directory.  Returns CLOUDSC_OK or CLOUDSC_EIO / ENOMEM. */
 int cloudsc_io_load_raw(const char *dir, int with_reference, cloudsc_dataset_t *ds);
 
+/* Load from a Serialbox store -- the reference's own data/ directory:
+ * MetaData-input.json (KLON/KLEV + parameters in global_meta_info, dims and
+ * types in field_map), ArchiveMetaData-input.json (offsets) and
+ * input_<FIELD>.dat; reference outputs from the "reference" prefix. */
+int cloudsc_io_load_serialbox(const char *dir, int with_reference, cloudsc_dataset_t *ds);
+
+/* A data directory: a Serialbox store if it holds MetaData-input.json, else
+ * the raw form (manifest.json + params.txt). */
+int cloudsc_io_load_dir(const char *dir, int with_reference, cloudsc_dataset_t *ds);
+
 /* Load from HDF5 files (reference_h5 may be NULL).  CLOUDSC_EIO if libhdf5
  * cannot be loaded or a file / dataset is missing; errors are described in
  * cloudsc_io_last_error(). */

@@ -268,13 +268,17 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     const real pap_k = in.pap;
     // saturation values (:583-609)
     const real e_liq = exp_liq<real>(c, ztp1), e_ice = exp_ice<real>(c, ztp1);
-    const real zfoeewmt = fmin(cl_div((c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)), pap_k), R(0.5));
-    const real zqsmix = cl_div(zfoeewmt, (R(1.0) - c.retv * zfoeewmt));
+    // divisors shared by several divisions (cl_recip: one reciprocal, same quotient bits)
+    const Recip<real> r_pap = cl_recip(pap_k);
+    const real zfoeewmt = fmin(cl_div((c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)), r_pap), R(0.5));
+    const Recip<real> r_mixd = cl_recip(R(1.0) - c.retv * zfoeewmt);
+    const real zqsmix = cl_div(zfoeewmt, r_mixd);
     const real zalfa_d = fmax(R(0.0), copysign(R(1.0), ztp1 - c.rtt));
-    real zfoeew = fmin(cl_div((zalfa_d * (c.r2es * e_liq) + (R(1.0) - zalfa_d) * (c.r2es * e_ice)), pap_k), R(0.5));
+    real zfoeew = fmin(cl_div((zalfa_d * (c.r2es * e_liq) + (R(1.0) - zalfa_d) * (c.r2es * e_ice)), r_pap), R(0.5));
     zfoeew = fmin(R(0.5), zfoeew);
-    const real zqsice = cl_div(zfoeew, (R(1.0) - c.retv * zfoeew));
-    const real zfoeeliqt = fmin(cl_div((c.r2es * e_liq), pap_k), R(0.5));
+    const Recip<real> r_iced = cl_recip(R(1.0) - c.retv * zfoeew);
+    const real zqsice = cl_div(zfoeew, r_iced);
+    const real zfoeeliqt = fmin(cl_div((c.r2es * e_liq), r_pap), R(0.5));
     const real zqsliq = cl_div(zfoeeliqt, (R(1.0) - c.retv * zfoeeliqt));
     // liquid/ice fractions (:628-636)
     const real zli = zqx[QL] + zqx[QI];
@@ -313,15 +317,16 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     real zfacw, zfaci, zfac, zcor;
     { const real d = ztp1 - c.r4les; zfacw = cl_div(c.r5les, (d * d)); }
     { const real d = ztp1 - c.r4ies; zfaci = cl_div(c.r5ies, (d * d)); }
-    zcor = cl_div(R(1.0), (R(1.0) - c.retv * zfoeew));
+    zcor = cl_div(R(1.0), r_iced);
     const real zdqsicedt = (zfaci * zcor) * zqsice;
     const real zcorqsice = R(1.0) + c.ralsdcp * zdqsicedt;
     zfac = zfoealfa * zfacw + (R(1.0) - zfoealfa) * zfaci;
-    zcor = cl_div(R(1.0), (R(1.0) - c.retv * zfoeewmt));
+    zcor = cl_div(R(1.0), r_mixd);
     const real zdqsmixdt = (zfac * zcor) * zqsmix;
     const real zcorqsmix = R(1.0) + (zfoealfa * c.ralvdcp + (R(1.0) - zfoealfa) * c.ralsdcp) * zdqsmixdt;
     const real zevaplimmix = fmax(cl_div((zqsmix - zqx[QV]), zcorqsmix), R(0.0));
     real ztmpa = cl_div(R(1.0), fmax(za, zepsec));
+    const Recip<real> r_1mza = cl_recip(fmax(zepsec, R(1.0) - za));
     real zliqcld = zqx[QL] * ztmpa;
     real zicecld = zqx[QI] * ztmpa;
     real zlicld = zliqcld + zicecld;
@@ -432,7 +437,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // 3.4 condensation/evaporation due to dqsat/dt: two Newton steps (:1137-1182)
     real zdqs;
     {
-      const real zdtdp = cl_div((c.zrdcp * ztp1), pap_k);
+      const real zdtdp = cl_div((c.zrdcp * ztp1), r_pap);
       const real zdpmxdt = zdp * c.zqtmst;
       const real zmfdn = (k < klev - 1) ? nb.pmfu_n + nb.pmfd_n : R(0.0);
       real zwtot = in.pvervel + c.half_rg * (nb.pmfu_k + nb.pmfd_k + zmfdn);
@@ -442,7 +447,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       const real zdtforc = (zdtdp * zwtot) * c.ptsphy + zdtdiab;
       real tt = fmax(ztp1 + zdtforc, R(160.0));
       real qsm = zqsmix;
-      const real zqp = cl_div(R(1.0), pap_k);
+      const real zqp = cl_div(R(1.0), r_pap);
   #pragma unroll
       for (int it = 0; it < 2; it++) {
         const real a = foealfa<real>(c, tt);
@@ -492,7 +497,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
       real zqe = R(0.0);
       if (c.nssopt == 0 || c.nssopt == 1) {
-        zqe = cl_div((zqx[QV] - za * zqsice), fmax(zepsec, R(1.0) - za));
+        zqe = cl_div((zqx[QV] - za * zqsice), r_1mza);
         zqe = fmax(R(0.0), zqe);
       } else if (c.nssopt == 2) {
         zqe = zqx[QV];
@@ -665,7 +670,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
 
     // 4.5 evaporation of rain, Abel and Boutle (:1982-2040)
-    const real zzrh0 = fmin(fmax(c.rprecrhmax + cl_div(((R(1.0) - c.rprecrhmax) * cs.zcovpmax), fmax(zepsec, R(1.0) - za)),
+    const real zzrh0 = fmin(fmax(c.rprecrhmax + cl_div(((R(1.0) - c.rprecrhmax) * cs.zcovpmax), r_1mza),
                                  c.rprecrhmax), R(1.0));
     {
       const real zzrh = fmin(R(0.8), zzrh0);
@@ -691,7 +696,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // 4.5 evaporation of snow, Sundqvist (:2048-2087)
     {
       const real zzrh = zzrh0;
-      real zqe = cl_div((zqx[QV] - za * zqsice), fmax(zepsec, R(1.0) - za));
+      real zqe = cl_div((zqx[QV] - za * zqsice), r_1mza);
       zqe = fmax(R(0.0), fmin(zqe, zqsice));
       if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) {
         const real x = cs.zcovptot * zdtgdp;
@@ -794,8 +799,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       const real d_s = R(1.0) + fsink_s;
       // off-diagonals zqlhs[ql][qs] = -sb_ls, zqlhs[qi][qs] = -sb_is; LU scales row-wise by
       // the pivot of the eliminating column: zqlhs[n][m] /= zqlhs[n][n] for m > n.
-      const real u_ls = cl_div((-sb_ls), d_l);    // zqlhs[ql][qs] after jn = ql
-      const real u_is = cl_div((-sb_is), d_i);    // zqlhs[qi][qs] after jn = qi
+      const Recip<real> r_dl = cl_recip(d_l), r_di = cl_recip(d_i);
+      const real u_ls = cl_div((-sb_ls), r_dl);    // zqlhs[ql][qs] after jn = ql
+      const real u_is = cl_div((-sb_is), r_di);    // zqlhs[qi][qs] after jn = qi
       // forward substitution (step 1): zqxn[qs] -= zqlhs[ql][qs]*zqxn[ql] + zqlhs[qi][qs]*zqxn[qi]
       qn_s = qn_s - u_ls * qn_l;
       qn_s = qn_s - u_is * qn_i;
@@ -804,8 +810,8 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       // (signed zeros and NaN included), so the division is dropped
       qn_s = cl_div(qn_s, d_s);
       qn_r = cl_div(qn_r, d_r);
-      qn_i = cl_div(qn_i, d_i);
-      qn_l = cl_div(qn_l, d_l);
+      qn_i = cl_div(qn_i, r_di);
+      qn_l = cl_div(qn_l, r_dl);
       // no small values (:2402-2412)
       if (qn_l < zepsec) { qn_v = qn_v + qn_l; qn_l = R(0.0); }
       if (qn_i < zepsec) { qn_v = qn_v + qn_i; qn_i = R(0.0); }

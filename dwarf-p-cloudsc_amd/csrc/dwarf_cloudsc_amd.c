@@ -357,7 +357,7 @@ int main(int argc, char **argv) {
     char dir[PATH_MAX];
     if (o.data_dir) snprintf(dir, sizeof(dir), "%s", o.data_dir);
     else default_data_dir(dir, sizeof(dir));
-    rc = cloudsc_io_load_raw(dir, 1, &ds);
+    rc = cloudsc_io_load_dir(dir, 1, &ds);
     if (!rc && o.reference_h5) {
       rc = cloudsc_io_load_hdf5_reference(o.reference_h5, &ds);     /* raw inputs, HDF5 reference */
       if (!rc) {

@@ -44,6 +44,8 @@ def io():
         subprocess.check_call(["make", "-s", "-C", PKG, "libcloudsc_io.so"])
     lib = C.CDLL(IO_LIB)
     lib.cloudsc_io_load_raw.argtypes = [C.c_char_p, C.c_int, C.POINTER(Dataset)]
+    lib.cloudsc_io_load_serialbox.argtypes = [C.c_char_p, C.c_int, C.POINTER(Dataset)]
+    lib.cloudsc_io_load_dir.argtypes = [C.c_char_p, C.c_int, C.POINTER(Dataset)]
     lib.cloudsc_io_load_hdf5.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Dataset)]
     lib.cloudsc_io_load_hdf5_reference.argtypes = [C.c_char_p, C.POINTER(Dataset)]
     lib.cloudsc_io_write_hdf5.argtypes = [C.POINTER(Dataset), C.c_char_p, C.c_char_p]
@@ -232,3 +234,89 @@ def test_host_expand_and_stats_match_python(io, ds):
         got = (st.minval, st.maxval, st.maxerr, st.errsum, st.refsum)
         assert got[:3] == tuple(want[:3]), key
         assert got[3] == pytest.approx(want[3], rel=1e-12) and got[4] == pytest.approx(want[4], rel=1e-12), key
+
+
+# ---- Serialbox store (the reference's data/ directory) ----
+REF_DATA_UPSTREAM = "/root/reference/data"
+
+
+def load_serialbox(io, path):
+    d = Dataset()
+    rc = io.cloudsc_io_load_serialbox(path.encode(), 1, C.byref(d))
+    assert rc == 0, io.cloudsc_io_last_error()
+    return d
+
+
+def assert_same_dataset(a: Dataset, b: Dataset):
+    assert (a.klon, a.klev) == (b.klon, b.klev)
+    ia, ra = arrays(a)
+    ib, rb = arrays(b)
+    assert sorted(ia) == sorted(ib) and sorted(ra) == sorted(rb)
+    for k in ia:
+        assert ia[k].dtype == ib[k].dtype and np.array_equal(ia[k], ib[k]), k
+    for k in ra:
+        assert np.array_equal(ra[k], rb[k]), k
+    pa, pb = a.params.to_dict(), b.params.to_dict()
+    assert pa == pb, {k: (pa[k], pb[k]) for k in pa if pa[k] != pb[k]}
+
+
+def test_serialbox_reader_equals_committed_conversion(io):
+    """data/cloudsc100 is a Serialbox store (the reference's MetaData-*.json,
+    ArchiveMetaData-*.json and .dat arrays): reading it natively gives exactly the
+    dataset of the committed conversion (manifest.json + params.txt), every array
+    and every parameter bit for bit (serialbox2hdf5/serialbox2hdf5.py:11-33 is the
+    reference's converter; load_state.c:538-690 its reader of the result)."""
+    a, b = load_serialbox(io, DATA), load_raw(io, DATA)
+    try:
+        assert_same_dataset(a, b)
+        assert a.has_reference and b"Serialbox" in a.source
+    finally:
+        io.cloudsc_io_free(C.byref(a))
+        io.cloudsc_io_free(C.byref(b))
+
+
+def test_serialbox_reader_on_the_reference_data_dir(io):
+    """`--data /root/reference/data`: the reference's own directory, unconverted."""
+    if not os.path.exists(os.path.join(REF_DATA_UPSTREAM, "MetaData-input.json")):
+        pytest.skip("no reference checkout")
+    a, b = load_serialbox(io, REF_DATA_UPSTREAM), load_raw(io, DATA)
+    try:
+        ia, _ = arrays(a)
+        # the reference directory also holds the two aerosol inputs the kernel never reads
+        assert {"plcrit_aer", "pccn"} <= set(ia)
+        for k in ("plcrit_aer", "pccn"):
+            a.inp[INPUT_NAMES.index(k)] = C.POINTER(C.c_double)()
+        assert_same_dataset(a, b)
+    finally:
+        io.cloudsc_io_free(C.byref(b))
+
+
+def test_load_dir_dispatch_and_errors(io, tmp_path):
+    d = Dataset()
+    assert io.cloudsc_io_load_dir(DATA.encode(), 1, C.byref(d)) == 0
+    assert b"Serialbox" in d.source
+    io.cloudsc_io_free(C.byref(d))
+    shutil.copytree(DATA, tmp_path / "sb")
+    # a field whose metadata disagrees with the file / the expected shape is rejected
+    with open(tmp_path / "sb" / "input_PAP.dat", "r+b") as fh:
+        fh.truncate(800)
+    assert io.cloudsc_io_load_serialbox(str(tmp_path / "sb").encode(), 1, C.byref(d)) == -6
+    assert b"input_PAP.dat" in io.cloudsc_io_last_error()
+    # a missing parameter scalar is an error, not a silent zero
+    import json
+    shutil.copy(os.path.join(DATA, "input_PAP.dat"), tmp_path / "sb" / "input_PAP.dat")
+    meta = json.load(open(tmp_path / "sb" / "MetaData-input.json"))
+    del meta["global_meta_info"]["YRECLDP_RTHOMO"]
+    os.chmod(tmp_path / "sb" / "MetaData-input.json", 0o644)
+    json.dump(meta, open(tmp_path / "sb" / "MetaData-input.json", "w"))
+    assert io.cloudsc_io_load_serialbox(str(tmp_path / "sb").encode(), 1, C.byref(d)) == -6
+    assert b"YRECLDP_RTHOMO" in io.cloudsc_io_last_error()
+
+
+def test_python_loader_reads_serialbox(ds):
+    """cloudsc_amd.load_dataset reads the Serialbox metadata too: same parameters
+    as params.txt (the committed conversion)."""
+    txt = ca.read_params_txt(os.path.join(DATA, "params.txt"))
+    sb = ca.read_serialbox_params(DATA)
+    assert txt == sb
+    assert ds.params == sb
