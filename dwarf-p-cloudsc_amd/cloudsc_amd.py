@@ -464,20 +464,22 @@ def validate_host_state(ds: "Dataset", st: "HostState") -> float:
     return worst
 
 
+# the translation unit of the CLOUDSC kernels (cloudsc_gpu.hip and what it includes)
+KERNEL_SOURCES = ("cloudsc_gpu.hip", "cloudsc_kcache.h", "cloudsc_scc.h", "cloudsc_dev.h", "cloudsc_params.h",
+                  "cloudsc_libm.h", "cloudsc_libm_tab.h", "cloudsc_internal.h")
+
+
 def kernel_source_hash() -> str:
-    """SHA-256 (16 hex digits) of the kernel sources and the library's build
-    flags: the key that ties a measured PMC traffic figure to the kernel it was
-    measured on (bench.py drops a figure whose hash is not the current one)."""
+    """SHA-256 (16 hex digits) of the kernels' sources and the library's build
+    flags (Makefile): the key that ties a measured PMC traffic figure to the
+    kernel it was measured on (bench.py drops a figure whose hash is not the
+    current one)."""
     import hashlib
     h = hashlib.sha256()
-    csrc = os.path.join(HERE, "csrc")
-    for name in sorted(os.listdir(csrc)):
-        if name.endswith((".hip", ".h")):
-            h.update(name.encode())
-            with open(os.path.join(csrc, name), "rb") as fh:
-                h.update(fh.read())
-    with open(os.path.join(HERE, "Makefile"), "rb") as fh:
-        h.update(fh.read())
+    for name in KERNEL_SOURCES + ("../../include/cloudsc_amd.h", "../Makefile"):
+        h.update(name.encode())
+        with open(os.path.normpath(os.path.join(HERE, "csrc", name)), "rb") as fh:
+            h.update(fh.read())
     return h.hexdigest()[:16]
 
 
