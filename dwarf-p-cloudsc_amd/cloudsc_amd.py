@@ -590,12 +590,24 @@ class HostPipeline:
     copies inputs in and outputs out, chunked and overlapped over streams."""
 
     def __init__(self, ds: Dataset, ngptot: int, nproma: int = 128, precision: int = FP64, device: int = 0,
-                 chunk_blocks: int = 32, nstreams: int = 4, col_offset: int = 0):
+                 chunk_blocks: int = 32, nstreams: int = 4, col_offset: int = 0, packed: bool = False):
+        """packed: all arrays carved back to back (8-byte gaps) out of ONE host
+        buffer, so that neighbouring fields share pages -- the layout that
+        exercises the pipeline's page-merged pinning."""
         self.lib = gpu_lib()
         self.ds, self.ngptot, self.nproma, self.precision = ds, ngptot, nproma, precision
         self._params = Params.from_dict(ds.params)
         check(self.lib.cloudsc_gpu_init(device, C.byref(self._params)))
         self.state = make_host_state(ds, ngptot, nproma, precision, col_offset)
+        if packed:
+            arrs = self.state.arrays
+            self._buf = np.empty(sum(a.nbytes + 8 for a in arrs.values()) + 64, dtype=np.uint8)
+            off = 8 - self._buf.ctypes.data % 8
+            for name, a in list(arrs.items()):
+                v = self._buf[off:off + a.nbytes].view(a.dtype).reshape(a.shape)
+                v[...] = a
+                arrs[name] = v
+                off += a.nbytes + 8
         self._plude0 = self.state.arrays["plude"].copy()
         f = self.state.fields()
         if not (ds.params.get("laericesed") or ds.params.get("laericeauto")):

@@ -2,8 +2,12 @@
 // (cloudsc_host_pipeline_*).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <vector>
+
+#include <unistd.h>
 
 #include "cloudsc_amd.h"
 #include "cloudsc_internal.h"
@@ -20,6 +24,15 @@ using namespace cloudsc_impl;
 // field, because the layout is block-major -- and chunk c runs on stream
 // c % nstreams: H2D of its inputs, the kernel, D2H of its outputs.  The host
 // arrays are pinned in place (hipHostRegister) once, at creation.
+//
+// Pinning is by whole pages, and arrays from a general-purpose allocator share
+// pages (the end of one field and the start of the next).  Registering each
+// array on its own then makes two registrations of one page; a copy of the
+// second array can be resolved against the first registration and run off its
+// end (a device page fault, seen in round 2 as "illegal memory access" in a
+// chunked SCC pipeline after other pipelines had come and gone).  So the page
+// ranges of all fields are merged first and every merged range is registered
+// once: each array lies wholly inside exactly one registration.
 namespace {
 
 enum FieldKind { FK_LEVEL, FK_HALF, FK_SPECIES, FK_SURFACE };
@@ -74,6 +87,66 @@ struct cloudsc_host_pipeline {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
+namespace {
+
+size_t field_bytes(const cloudsc_host_pipeline* p, int i, int nblocks) {
+  const FieldDesc& d = kFieldTable[i];
+  return (size_t)nblocks * per_block_elems(d.kind, p->nproma, p->klev) * (d.is_int ? sizeof(int) : p->es);
+}
+
+// [ptr, ptr+bytes) is host memory the device can reach as ONE mapping: both ends
+// resolve to pinned host memory at device addresses exactly bytes-1 apart
+bool pinned_as_one(const void* ptr, size_t bytes) {
+  hipPointerAttribute_t a, b;
+  if (hipPointerGetAttributes(&a, ptr) != hipSuccess ||
+      hipPointerGetAttributes(&b, (const char*)ptr + bytes - 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost && b.type == hipMemoryTypeHost && a.devicePointer && b.devicePointer &&
+         (const char*)b.devicePointer - (const char*)a.devicePointer == (ptrdiff_t)(bytes - 1);
+}
+
+// Pin the caller's arrays in place: the page ranges of all fields merged into
+// disjoint ranges, each registered once (see the note at the top).  A range the
+// caller has pinned already (hipHostMalloc, or its own hipHostRegister) is used
+// as it is if every field in it is covered by one mapping; otherwise the
+// pipeline refuses the arrays rather than risk a partial mapping.
+int pin_host_fields(cloudsc_host_pipeline* p, void* const* hf) {
+  const long sys_pg = sysconf(_SC_PAGESIZE);
+  const uintptr_t pg = sys_pg > 0 ? (uintptr_t)sys_pg : 4096;
+  struct Span { uintptr_t lo, hi; };
+  std::vector<Span> spans;
+  for (int i = 0; i < kNumFields; i++) {
+    if (!hf[i]) continue;
+    const uintptr_t a = (uintptr_t)hf[i], e = a + field_bytes(p, i, p->nblocks);
+    spans.push_back({a & ~(pg - 1), (e + pg - 1) & ~(pg - 1)});
+  }
+  std::sort(spans.begin(), spans.end(), [](const Span& x, const Span& y) { return x.lo < y.lo; });
+  std::vector<Span> merged;
+  for (const Span& s : spans) {
+    if (!merged.empty() && s.lo <= merged.back().hi) merged.back().hi = std::max(merged.back().hi, s.hi);
+    else merged.push_back(s);
+  }
+  for (const Span& s : merged) {
+    const hipError_t e = hipHostRegister((void*)s.lo, s.hi - s.lo, hipHostRegisterDefault);
+    if (e == hipSuccess) { p->pinned.push_back((void*)s.lo); continue; }
+    (void)hipGetLastError();
+    if (e != hipErrorHostMemoryAlreadyRegistered) return hip_fail(e, "hipHostRegister");
+    for (int i = 0; i < kNumFields; i++) {
+      const uintptr_t a = (uintptr_t)hf[i];
+      if (!hf[i] || a < s.lo || a >= s.hi) continue;
+      if (!pinned_as_one(hf[i], field_bytes(p, i, p->nblocks))) {
+        set_error_text("host pipeline: an array lies partly in memory pinned by the caller; pin all or none");
+        return CLOUDSC_EINVAL;
+      }
+    }
+  }
+  return CLOUDSC_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p);
@@ -98,16 +171,7 @@ int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int 
   // later cloudsc_gpu_init does to the device's default set
   if ((rc = param_set_copy(&p->params, device_default_params(device)))) return fail(rc);
   void* const* hf = (void* const*)&p->host;
-  // pin the caller's arrays in place (already-pinned memory is fine)
-  for (int i = 0; i < kNumFields; i++) {
-    if (!hf[i]) continue;
-    const FieldDesc& d = kFieldTable[i];
-    const size_t bytes = (size_t)p->nblocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : p->es);
-    hipError_t e = hipHostRegister(hf[i], bytes, hipHostRegisterDefault);
-    if (e == hipSuccess) p->pinned.push_back(hf[i]);
-    else if (e != hipErrorHostMemoryAlreadyRegistered) { hip_fail(e, "hipHostRegister"); return fail(CLOUDSC_EHIP); }
-    else (void)hipGetLastError();
-  }
+  if ((rc = pin_host_fields(p, hf))) return fail(rc);
   p->slots.resize(nstreams);
   for (auto& s : p->slots) {
     if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);

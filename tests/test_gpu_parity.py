@@ -328,6 +328,24 @@ def test_host_pipeline_equals_resident(lib, ds, variant, chunk, nstreams):
         assert np.array_equal(out[k], ref[k]), k
 
 
+@pytest.mark.parametrize("variant", [ca.VARIANT_SCC, ca.VARIANT_KSEG, ca.VARIANT_KCACHE])
+def test_host_pipeline_packed_arrays(lib, ds, variant):
+    """Host arrays carved back to back out of one buffer, so that neighbouring
+    fields share pages: the pipeline pins merged page ranges, every array lies
+    inside one registration, and the chunked run gives the resident bits.
+    (Pinning each array on its own faulted the device in round 2.)"""
+    ref = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KCACHE)
+    hp = ca.HostPipeline(ds, 1000, 128, chunk_blocks=5, nstreams=1, packed=True)
+    try:
+        hp.run(variant)
+        hp.run(variant)
+        out = hp.outputs()
+    finally:
+        hp.close()
+    for _, k in ca.VALIDATED:
+        assert np.array_equal(out[k], ref[k]), k
+
+
 def test_host_pipeline_fp32(lib, ds):
     ref = run_gpu(ds, 1000, 128, precision=ca.FP32)
     hp = ca.HostPipeline(ds, 1000, 128, precision=ca.FP32, chunk_blocks=4, nstreams=2)
