@@ -939,8 +939,9 @@ CLOUDSC_HD void init_carry(CS& cs) {
 // persistent kernel (below) runs a column in level segments.
 template <typename real, int PF, bool AER, typename CS>
 __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar, int b,
-                                              unsigned lo, int lev0, int lev1, CS& cs) {
-  if (lev0 >= lev1) return;                         // empty segment: no loads at lev0 (may be == klev)
+                                              unsigned lo0, int lev0, int lev1, CS& cs) {
+  if (lev0 >= lev1) return;
+  const unsigned lo = lo0;                         // empty segment: no loads at lev0 (may be == klev)
   // PF: 0 = loads at the top of their level, 1 = level k+1 prefetched into
   // registers, 2 = like 0, and the neighbour-level values (paph/pmfu/pmfd/plu of
   // k, k+1) re-read every level instead of carried (fewer live registers,
@@ -977,6 +978,10 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
     // the level index is laundered too, so no per-field induction pointers are formed
     int k = kloop;
     asm volatile("" : "+s"(k));
+    // and so is the lane's 32-bit byte offset: its zero-extension is then formed
+    // in this block, where the level loads fold it into the saddr + voffset form
+    // instead of a 64-bit VGPR address add per load
+    const unsigned lo = launder_vgpr(lo0);
     const bool physics = k >= ncldtop0;
     // ---- issue the loads of the next levels (software pipelining) ----
     real paph_nn, pmfu_nn, pmfd_nn, plu_nn;
