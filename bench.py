@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
     p.add_argument("--variant", choices=["kseg", "kcache", "scc"], default=None,
                    help="default: kseg for fp64 (2 waves/SIMD leave a tail the persistent kernel removes), "
-                        "kcache for fp32 (3-4 waves/SIMD, no tail)")
+                        "kcache for fp32 (measured faster than kseg in fp32: profiles/r02/fp32_cfg_sweep.jsonl)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--transfer", action="store_true",
                    help="also time the host-buffer path (H2D -> kernel -> D2H, chunked over streams): "
