@@ -40,7 +40,7 @@ def parse():
                    help="NPROMA (block = workgroup); 64 is the measured best for the persistent kernel "
                         "(profiles/r01/nproma_sweep_all_variants.jsonl)")
     p.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
-    p.add_argument("--variant", choices=["kseg", "kcache", "scc"], default=None,
+    p.add_argument("--variant", choices=["kseg", "kcache", "scc", "scc-private"], default=None,
                    help="default: kseg for fp64 (2 waves/SIMD leave a tail the persistent kernel removes), "
                         "kcache for fp32 (measured faster than kseg in fp32: profiles/r02/fp32_cfg_sweep.jsonl)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -151,7 +151,8 @@ def main():
     col_offset, ncols = cd.shard(rank, args.ngptot)
 
     prec = ca.FP64 if args.precision == "fp64" else ca.FP32
-    variant = {"kseg": ca.VARIANT_KSEG, "kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC}[args.variant]
+    variant = {"kseg": ca.VARIANT_KSEG, "kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC,
+               "scc-private": ca.VARIANT_SCC_PRIVATE}[args.variant]
     ds = ca.load_dataset()
     # one GPU per local rank (ranks beyond the device count share devices, e.g.
     # a 2-rank rehearsal on a 1-GPU box)
@@ -207,7 +208,8 @@ def main():
                 "expanded on the device with g % 100",
         "config": {"workload": "CLOUDSC %s, NGPTOT=%d per GPU, KLEV=%d, NPROMA=%d, %s" % (
             {ca.VARIANT_KSEG: "SCC-k-caching (persistent, level-segmented)",
-             ca.VARIANT_KCACHE: "SCC-k-caching", ca.VARIANT_SCC: "SCC (HBM temporaries)"}[variant],
+             ca.VARIANT_KCACHE: "SCC-k-caching", ca.VARIANT_SCC: "SCC (HBM temporaries)",
+             ca.VARIANT_SCC_PRIVATE: "SCC (per-thread private-array temporaries)"}[variant],
             args.ngptot, ds.klev, args.nproma, args.precision),
             "ngptot_per_gpu": args.ngptot, "ngptot_total": total_cols, "klev": ds.klev,
             "nproma": args.nproma, "variant": args.variant, "parallelism": "columns sharded, %d GPU(s)" % world},

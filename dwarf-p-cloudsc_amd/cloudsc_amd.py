@@ -35,7 +35,7 @@ DATA_DIR = os.path.join(REPO, "data", "cloudsc100")   # the reference's data/ ar
 
 NCLV = 5
 FP64, FP32 = 8, 4
-VARIANT_SCC, VARIANT_KCACHE, VARIANT_KSEG = 1, 2, 3
+VARIANT_SCC, VARIANT_KCACHE, VARIANT_KSEG, VARIANT_SCC_PRIVATE = 1, 2, 3, 4
 
 # ---------------------------------------------------------------------------
 # cloudsc_params_t  (order == include/cloudsc_amd.h)

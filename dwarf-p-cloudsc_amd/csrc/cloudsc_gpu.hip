@@ -195,6 +195,13 @@ __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccS
   const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
   cloudsc_scc_body<real, AER>(ka, s, params_of<real>(ka));
 }
+template <typename real, bool AER>
+__global__ void __launch_bounds__(256) scc_private_entry(const KArgs<real> a) {
+  (void)a;
+  libm_tables_to_lds<real>();
+  const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
+  cloudsc_scc_private_body<real, AER>(ka, params_of<real>(ka));
+}
 
 // ---------------------------------------------------------------------------
 // launch helpers
@@ -414,6 +421,10 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
       hipLaunchKernelGGL(kseg_prepare_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, (unsigned*)scratch, nflags);
     }
     rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems) : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems);
+  } else if (variant == CLOUDSC_VARIANT_SCC_PRIVATE) {
+    if (klev > kPrivKlev) return CLOUDSC_EINVAL;    // the private arrays are sized at compile time
+    if (aer) hipLaunchKernelGGL((scc_private_entry<real, true>), dim3(nblocks), dim3(nproma), 0, st, a);
+    else hipLaunchKernelGGL((scc_private_entry<real, false>), dim3(nblocks), dim3(nproma), 0, st, a);
   } else {
     if (!scratch) return CLOUDSC_EINVAL;
     SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
@@ -456,8 +467,8 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t* params) {
 }
 
 long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev) {
-  if (variant == CLOUDSC_VARIANT_KCACHE) return 0;
   if (ngptot <= 0 || nproma <= 0 || klev < 2) return -1;
+  if (variant == CLOUDSC_VARIANT_KCACHE || variant == CLOUDSC_VARIANT_SCC_PRIVATE) return 0;
   if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return -1;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
   if (variant == CLOUDSC_VARIANT_KSEG)
@@ -476,7 +487,8 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CLOUDSC_ENODEV;
   if (device < 0 || device >= n || device >= kMaxDevices) return CLOUDSC_ENODEV;
   if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return CLOUDSC_EINVAL;
-  if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC && variant != CLOUDSC_VARIANT_KSEG)
+  if (variant != CLOUDSC_VARIANT_KCACHE && variant != CLOUDSC_VARIANT_SCC && variant != CLOUDSC_VARIANT_KSEG &&
+      variant != CLOUDSC_VARIANT_SCC_PRIVATE)
     return CLOUDSC_EINVAL;
   // KCACHE and SCC run one workgroup of nproma threads per block; KSEG runs
   // 64-column sub-blocks of any block width

@@ -200,7 +200,8 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
   const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
   // workspaces for the chunk size (SCC / KSEG), allocated on first use
   for (auto& s : p->slots) {
-    if (variant == CLOUDSC_VARIANT_KCACHE || s.scratch_variant == variant) continue;
+    if (variant == CLOUDSC_VARIANT_KCACHE || variant == CLOUDSC_VARIANT_SCC_PRIVATE || s.scratch_variant == variant)
+      continue;
     const long long nb = cloudsc_gpu_scratch_bytes(p->precision, variant, p->chunk_blocks * p->nproma, p->nproma,
                                                    p->klev);
     if (nb <= 0) return CLOUDSC_EINVAL;

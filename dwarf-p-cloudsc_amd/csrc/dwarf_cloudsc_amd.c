@@ -75,6 +75,16 @@ typedef struct {
   cloudsc_stats_t stats[CLOUDSC_NVALID];
 } shard_t;
 
+static const char *variant_name(int v) {
+  switch (v) {
+    case CLOUDSC_VARIANT_KSEG: return "kseg";
+    case CLOUDSC_VARIANT_KCACHE: return "kcache";
+    case CLOUDSC_VARIANT_SCC: return "scc";
+    case CLOUDSC_VARIANT_SCC_PRIVATE: return "scc-private";
+    default: return "cpu";
+  }
+}
+
 static double now(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -86,7 +96,7 @@ static void usage(const char *prog) {
           "usage: %s [<nthreads> <ngptot> <nproma>] [options]\n"
           "  --gpus N              shard the columns over N devices (default 1)\n"
           "  --precision fp64|fp32 (default fp64)\n"
-          "  --variant kseg|kcache|scc|cpu (default kseg; cpu = the library's CPU variant on\n"
+          "  --variant kseg|kcache|scc|scc-private|cpu (default kseg; cpu = the library's CPU variant on\n"
           "                        <nthreads> host threads, host-memory fields: BASELINE config 1)\n"
           "  --reps R              timed steps (default 1)\n"
           "  --warmup W            untimed steps before the timed ones (default 1)\n"
@@ -127,6 +137,7 @@ static int parse(int argc, char **argv, options_t *o) {
       if (!strcmp(v, "kseg")) o->variant = CLOUDSC_VARIANT_KSEG;
       else if (!strcmp(v, "kcache")) o->variant = CLOUDSC_VARIANT_KCACHE;
       else if (!strcmp(v, "scc")) o->variant = CLOUDSC_VARIANT_SCC;
+      else if (!strcmp(v, "scc-private")) o->variant = CLOUDSC_VARIANT_SCC_PRIVATE;
       else if (!strcmp(v, "cpu")) o->variant = VARIANT_CPU;
       else { fprintf(stderr, "bad variant %s\n", v); return -1; }
     } else if (!strcmp(a, "--reps")) { NEEDV(); o->reps = atoi(v); }
@@ -407,7 +418,7 @@ int main(int argc, char **argv) {
   if (o.transfer) {
     printf(" CLOUDSC-AMD: %s, variant %s, host-buffer path (--transfer), 1 device; state: %s\n",
            o.precision == CLOUDSC_FP64 ? "fp64" : "fp32",
-           o.variant == CLOUDSC_VARIANT_KSEG ? "kseg" : o.variant == CLOUDSC_VARIANT_KCACHE ? "kcache" : "scc",
+           variant_name(o.variant),
            ds.source);
     rc = run_host(&o, &ds);
     cloudsc_io_free(&ds);
@@ -421,7 +432,7 @@ int main(int argc, char **argv) {
   const int nblocks = o.ngptot / o.nproma + (o.ngptot % o.nproma ? 1 : 0);
   printf(" CLOUDSC-AMD: %s, variant %s, %d device(s); state: %s (KLON=%d, KLEV=%d)\n",
          o.precision == CLOUDSC_FP64 ? "fp64" : "fp32",
-         o.variant == CLOUDSC_VARIANT_KSEG ? "kseg" : o.variant == CLOUDSC_VARIANT_KCACHE ? "kcache" : "scc",
+         variant_name(o.variant),
          o.ngpus, ds.source, ds.klon, ds.klev);
 
   /* ---- shard: block-aligned contiguous ranges of the global column index ---- */

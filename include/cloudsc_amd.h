@@ -65,6 +65,9 @@ extern "C" {
 #define CLOUDSC_VARIANT_KCACHE 2   /* SCC-k-caching: one fused level loop, carried state in registers       */
 #define CLOUDSC_VARIANT_KSEG   3   /* SCC-k-caching, persistent work queue over (level segment, block)      */
                                    /* items; carried state handed between segments through HBM scratch   */
+#define CLOUDSC_VARIANT_SCC_PRIVATE 4  /* SCC with per-thread private-array temporaries (scratch memory):   */
+                                   /* the reference CUDA SCC form, cloudsc_c.cu:60-317; klev <= 137 as    */
+                                   /* there (:53); no caller workspace                                     */
 
 /* error codes */
 #define CLOUDSC_OK            0
@@ -148,6 +151,8 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t *params);
  * NULL for the default stream) of `device`.  Asynchronous; errors in the launch
  * configuration are returned, asynchronous faults surface at the caller's sync.
  * SCC and KSEG need a workspace: pass scratch of cloudsc_gpu_scratch_bytes()
+ * (KCACHE and SCC_PRIVATE need none: the latter's temporaries are the
+ * kernel's private segment, sized by the HIP runtime at launch)
  * bytes (NULL is fine for KCACHE).  The KSEG workspace holds a dequeue counter
  * and per-block flags that are re-zeroed on `stream` before every launch, so one
  * workspace must not be shared by launches in flight on different streams.

@@ -65,6 +65,7 @@ def test_strerror_and_scratch_sizes(lib):
     assert b"hand-off" in lib.cloudsc_strerror(-7)
     # KCACHE needs no workspace; SCC and KSEG do; bad sizes -> -1
     assert lib.cloudsc_gpu_scratch_bytes(ca.FP64, ca.VARIANT_KCACHE, 163840, 128, 137) == 0
+    assert lib.cloudsc_gpu_scratch_bytes(ca.FP64, ca.VARIANT_SCC_PRIVATE, 163840, 128, 137) == 0
     kseg = lib.cloudsc_gpu_scratch_bytes(ca.FP64, ca.VARIANT_KSEG, 163840, 128, 137)
     assert kseg >= 1280 * 19 * 128 * 8
     assert lib.cloudsc_gpu_scratch_bytes(ca.FP32, ca.VARIANT_KSEG, 163840, 128, 137) < kseg

@@ -170,6 +170,19 @@ def test_bitwise_scc_full_size(lib, ds):
     assert bitwise_mismatches(scc, kc) == {}
 
 
+def test_bitwise_scc_private_full_size(lib, ds):
+    """The reference's own SCC form (per-thread private arrays, cloudsc_c.cu:60-317)
+    at the full 163840 columns / NPROMA 128: 28.5 KB of private segment per
+    thread -- bit-equal to KCACHE on the same state."""
+    g = ca.GpuState(ds, 163840, 128)
+    try:
+        scp = outputs_of(g, ca.VARIANT_SCC_PRIVATE)
+        kc = outputs_of(g, ca.VARIANT_KCACHE)
+    finally:
+        g.close()
+    assert bitwise_mismatches(scp, kc) == {}
+
+
 def test_bitwise_fp32_full_size(lib, ds, oracle_mod):
     """BASELINE.json config 4: SCC-k-caching fp32, NGPTOT 163840 (NPROMA 64, the
     fp32 bench default) -- bit-equal to the fp32 restatement at the same size;

@@ -138,6 +138,28 @@ def test_scc_scenarios(lib, scenarios, name):
     assert_close(field_report(out, s.reference), RELL1_FP64, MAXREL_FP64, "scc scenario %s" % name)
 
 
+# ---- SCC with per-thread private-array temporaries (the reference's cloudsc_c.cu form, a3) ----
+@pytest.mark.parametrize("precision", [ca.FP64, ca.FP32])
+def test_scc_private_equals_kcache_bitwise(lib, ds, precision):
+    a = run_gpu(ds, 1000, 128, precision=precision, variant=ca.VARIANT_KCACHE)
+    b = run_gpu(ds, 1000, 128, precision=precision, variant=ca.VARIANT_SCC_PRIVATE)
+    for _, k in ca.VALIDATED:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_scc_private_klev_bound(lib, ds):
+    """The private arrays are sized for the reference's klev = 137: more levels is EINVAL."""
+    import ctypes as C
+    g = ca.GpuState(ds, 256, 128)
+    try:
+        f = ca.Fields()
+        ca.check(lib.cloudsc_state_fields(g.h, C.byref(f)))
+        assert lib.cloudsc_gpu_run(0, None, ca.FP64, ca.VARIANT_SCC_PRIVATE, 256, 128, 138, C.byref(f), None) == -1
+        ca.check(lib.cloudsc_state_sync(g.h))
+    finally:
+        g.close()
+
+
 def test_shard_offset_bitwise(lib, ds):
     # a shard starting at global column 384 reproduces the tail of the full run
     full = run_gpu(ds, 1024, 128)
@@ -312,7 +334,8 @@ def test_aerosol_flags_vs_oracle(lib, ds, oracle_mod, variant):
 
 # ---- host-buffer pipeline (H2D -> kernel -> D2H, chunked over streams) ----
 @pytest.mark.parametrize("variant,chunk,nstreams", [(ca.VARIANT_KCACHE, 3, 2), (ca.VARIANT_KSEG, 2, 3),
-                                                     (ca.VARIANT_SCC, 5, 1), (ca.VARIANT_KCACHE, 100, 4)])
+                                                     (ca.VARIANT_SCC, 5, 1), (ca.VARIANT_KCACHE, 100, 4),
+                                                     (ca.VARIANT_SCC_PRIVATE, 3, 2)])
 def test_host_pipeline_equals_resident(lib, ds, variant, chunk, nstreams):
     """Chunks of a few blocks (the last one partial, with the partial last
     block) give the same bits as the device-resident run."""
@@ -475,7 +498,7 @@ def test_wide_blocks_rejected_outside_kseg(lib, ds):
 
 
 @pytest.mark.parametrize("name", ["W", "M"])
-@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE])
 def test_bitwise_vs_reference_kernel_scenarios(lib, scenarios, name, variant):
     s = scenarios[name]
     out = run_gpu(s, 100, 128, variant=variant)

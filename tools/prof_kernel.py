@@ -21,6 +21,7 @@ if a.cfg:
     os.environ["CLOUDSC_KCACHE_CFG"] = a.cfg
 ds = ca.load_dataset()
 g = ca.GpuState(ds, a.ngptot, a.nproma, ca.FP64 if a.precision == "fp64" else ca.FP32)
-ms = g.run({"kseg": ca.VARIANT_KSEG, "kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC}[a.variant], a.reps)
+ms = g.run({"kseg": ca.VARIANT_KSEG, "kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC,
+      "scc-private": ca.VARIANT_SCC_PRIVATE}[a.variant], a.reps)
 print("kernel ms:", ms)
 g.close()

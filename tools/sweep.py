@@ -43,7 +43,8 @@ def main():
                         os.environ[key] = val
                     else:
                         os.environ.pop(key, None)
-                var = {"kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC, "kseg": ca.VARIANT_KSEG}[var_s]
+                var = {"kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC, "kseg": ca.VARIANT_KSEG,
+               "scc-private": ca.VARIANT_SCC_PRIVATE}[var_s]
                 g.run(var, a.warmup)
                 ms = g.run(var, a.reps)
                 med = float(np.median(ms))
