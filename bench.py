@@ -158,6 +158,14 @@ def main():
     # a 2-rank rehearsal on a 1-GPU box)
     device = topo.local_rank % ca.device_count()
     g = ca.GpuState(ds, ncols, args.nproma, prec, device=device, col_offset=col_offset)
+    # The achievable-HBM (STREAM copy) measurement runs first: ~0.1 s of heavy
+    # GPU work, after which the shader clock has left its idle level.  The
+    # kernel's time follows the clock (profiles/r02/clock_probe_kseg_fp64.json:
+    # 1.95 ms at 1.85 GHz for the first dispatches of a cold device, 1.68 ms at
+    # 2.3 GHz once ramped), so a cold start would otherwise bias the first steps.
+    peak_meas = None
+    if not args.no_hbm_peak:          # every rank warms its own device the same way
+        peak_meas = ca.hbm_copy_gbps(device, 4 << 30, 10)
 
     if args.warmup > 0:
         g.run(variant, args.warmup)
@@ -189,9 +197,6 @@ def main():
     achieved = bpc * args.ngptot / (k_avg_ms * 1e-3) / 1e9
     traffic, traffic_src = roofline_traffic(
         ca, args.traffic_json, "%s_%s_%d_%d" % (args.variant, args.precision, args.ngptot, args.nproma))
-    peak_meas = None
-    if not args.no_hbm_peak:
-        peak_meas = ca.hbm_copy_gbps(device, 4 << 30, 10)
     line = {
         "metric": "grid-columns/sec at NGPTOT=163840 KLEV=137 fp64; achieved HBM GB/s vs peak",
         "value": round(value, 1),

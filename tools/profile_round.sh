@@ -8,8 +8,11 @@ R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 out=$R/gpurun_out/prof
 mkdir -p $out
+# the FETCH pass also counts GRBM_GUI_ACTIVE (GPU busy cycles, summed over the 8 XCDs): with the
+# dispatch durations of the same pass it gives the effective shader clock of the box
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d $out/pmc_${c}_${variant}_${prec} -o run --output-format csv \
+  pmc=$c; [ $c == FETCH_SIZE ] && pmc="FETCH_SIZE GRBM_GUI_ACTIVE"
+  timeout -k 10 300 rocprofv3 --pmc $pmc --kernel-trace -d $out/pmc_${c}_${variant}_${prec} -o run --output-format csv \
     -- python3 $R/tools/prof_kernel.py --variant $variant --precision $prec --nproma $nproma --reps 3 \
     > $out/pmc_${c}_${variant}_${prec}.log 2>&1 || exit $?
 done
