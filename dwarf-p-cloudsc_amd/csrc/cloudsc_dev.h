@@ -124,6 +124,12 @@ typedef double cl_f64x2 __attribute__((ext_vector_type(2)));
 __shared__ cl_u64x2 s_cl_exp_tab[128];       // {tail, sbits}
 __shared__ cl_f64x2 s_cl_log_tab[128];       // {invc, logc}
 __shared__ double s_cl_logtail_tab[128];     // logctail
+// the addends of the polynomials' two-constant fmas: {C4, C2} of exp, {A5, A3, A1, -} of log.
+// Read from LDS (one ds_read_b128 per exp, two per log), they arrive in VGPRs without VALU
+// moves; a VOP3 fma reads at most one scalar and no literal, so one of the two constants of
+// fma(r, C5, C4) has to come from a VGPR.  (The plain exp table read is already waited for
+// right there, so the extra LDS latency hides under it.)
+__shared__ cl_f64x2 s_cl_poly[3];
 // single precision (expf/powf): 32 x 2^(i/32) bits, 16 x {invc, logc}
 __constant__ __attribute__((aligned(16))) unsigned long long g_cl_exp2f_tab[32] = {CLOUDSC_LIBM_EXP2F_TAB};
 __constant__ __attribute__((aligned(16))) double g_cl_powf_tab[2 * 16] = {CLOUDSC_LIBM_POWF_LOG2_TAB};
@@ -145,6 +151,14 @@ struct ConstLibmTabsF {
   }
 };
 struct LdsLibmTabs {
+  __device__ __forceinline__ cloudsc_libm::ExpAddends exp_addends() const {
+    const cl_f64x2 a = s_cl_poly[0];
+    return {a.x, a.y};
+  }
+  __device__ __forceinline__ cloudsc_libm::LogAddends log_addends() const {
+    const cl_f64x2 a = s_cl_poly[1], b = s_cl_poly[2];
+    return {a.x, a.y, b.x};
+  }
   __device__ __forceinline__ cloudsc_libm::ExpEntry exp_entry(uint32_t k) const {
     const cl_u64x2 e = s_cl_exp_tab[k];
     return {e.x, e.y};
@@ -157,6 +171,12 @@ struct LdsLibmTabs {
 // The complete functions, out of line, for the arguments outside the hot
 // range (tables from __constant__ memory; never taken by CLOUDSC's data).
 struct ConstLibmTabs {
+  __device__ __forceinline__ cloudsc_libm::ExpAddends exp_addends() const {
+    return {cloudsc_libm::kC4, cloudsc_libm::kC2};
+  }
+  __device__ __forceinline__ cloudsc_libm::LogAddends log_addends() const {
+    return {cloudsc_libm::kA5, cloudsc_libm::kA3, cloudsc_libm::kA1};
+  }
   __device__ __forceinline__ cloudsc_libm::ExpEntry exp_entry(uint32_t k) const {
     const cl_u64x2 e = ((const cl_u64x2*)g_cl_exp_tab)[k];
     return {e.x, e.y};
@@ -190,6 +210,11 @@ __device__ __forceinline__ void libm_tables_to_lds() {
       s_cl_exp_tab[i] = ((const cl_u64x2*)g_cl_exp_tab)[i];
       s_cl_log_tab[i] = ((const cl_f64x2*)g_cl_log_tab)[2 * i];
       s_cl_logtail_tab[i] = g_cl_log_tab[4 * i + 2];
+    }
+    if (threadIdx.x == 0) {
+      s_cl_poly[0] = cl_f64x2{cloudsc_libm::kC4, cloudsc_libm::kC2};
+      s_cl_poly[1] = cl_f64x2{cloudsc_libm::kA5, cloudsc_libm::kA3};
+      s_cl_poly[2] = cl_f64x2{cloudsc_libm::kA1, 0.0};
     }
     __syncthreads();
   } else {

@@ -4,7 +4,7 @@
 #   tools/ab_time.sh "<sweep args>" lib1.so lib2.so ...   (interleaved, 2 rounds)
 args=$1; shift
 mkdir -p gpurun_out
-for round in 1 2; do
+for round in $(seq 1 ${ROUNDS:-2}); do
   for lib in "$@"; do
     tag=$(basename $lib .so)
     CLOUDSC_AMD_LIB=$(realpath $lib) timeout -k 10 300 python tools/sweep.py $args --reps 20 > gpurun_out/abt_${tag}_$round.log 2>&1 || exit $?
