@@ -76,16 +76,15 @@ __device__ __forceinline__ void scc_get_ls(const real* base, size_t idx, size_t 
 template <typename real>
 struct HbmTemps {
   SccScratch<real> S;
-  size_t ulsb, uqxb, upfb, plane, pstride;
+  size_t plane, pstride, ulsb, uqxb, upfb;
+  int nproma_;
   unsigned lo;
   __device__ __forceinline__ HbmTemps(const SccScratch<real>& s, int b, int nproma, int klev, unsigned lane)
-      : S(s), plane((size_t)klev * nproma), pstride((size_t)(klev + 1) * nproma), lo(lane) {
-    ulsb = (size_t)b * kSccLsPlanes * plane;     // S.ls     [planes][klev][nproma]
-    uqxb = (size_t)b * 4 * plane;                // S.qxn    [4][klev][nproma]
-    upfb = (size_t)b * 3 * pstride;              // S.pfx    [3][klev+1][nproma]
-    nproma_ = nproma;
-  }
-  int nproma_;
+      : S(s), plane((size_t)klev * nproma), pstride((size_t)(klev + 1) * nproma),
+        ulsb((size_t)b * kSccLsPlanes * plane),   // S.ls  [planes][klev][nproma]
+        uqxb((size_t)b * 4 * plane),              // S.qxn [4][klev][nproma]
+        upfb((size_t)b * 3 * pstride),            // S.pfx [3][klev+1][nproma]
+        nproma_(nproma), lo(lane) {}
   __device__ __forceinline__ void put_ls(int k, const LevelState<real>& ls) {
     scc_put_ls(S.ls, ulsb + (size_t)k * nproma_, plane, lo, ls);
   }

@@ -2,14 +2,19 @@
 # Effective shader clock of this box while the fp64 KSEG kernel runs: one
 # rocprofv3 pass counting GRBM_GUI_ACTIVE (busy cycles, summed over the 8 XCDs)
 # with the kernel trace of the same dispatches -> gpurun_out/clock_probe.json
-# (kernel ms and GHz per dispatch).  usage: tools/clock_probe.sh [reps]
+# (kernel ms and GHz per dispatch).  usage: tools/clock_probe.sh [reps] [-- program args...]
+# (with "-- bench.py ...": the clock of every KSEG dispatch of that bench run)
 reps=${1:-10}
+shift
+[ "$1" == "--" ] && shift
+prog=("$@")
+[ ${#prog[@]} -eq 0 ] && prog=(tools/prof_kernel.py --variant kseg --precision fp64 --nproma 64 --reps $reps)
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 out=$R/gpurun_out/clock_probe
 rm -rf $out && mkdir -p $out
 timeout -k 10 120 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace -d $out -o run --output-format csv \
-  -- python3 $R/tools/prof_kernel.py --variant kseg --precision fp64 --nproma 64 --reps $reps > $out/run.log 2>&1 || exit $?
+  -- python3 $R/"${prog[0]}" "${prog[@]:1}" > $out/run.log 2>&1 || exit $?
 python3 - "$out" <<'PY'
 import csv, glob, json, os, re, sys
 d = sys.argv[1]

@@ -100,6 +100,25 @@ int main(int argc, char** argv) {
     }
     fail |= t.report();
   }
+  {  // the tiny range the split form runs through its hot path (|x| < 2^-54 incl. subnormals)
+    Tally t{"exp |x| < 2^-54"};
+    for (long long s = 0; s < M; ++s) {
+      const double x = ((s & 1) ? -1.0 : 1.0) * std::exp2(-1074.0 + 1020.0 * u01(rng));
+      t.add(split_exp(x), std::exp(x), x, 0);
+    }
+    for (double x : {0x1p-54, -0x1p-54, 0x1.fffffffffffffp-55, -0x1.fffffffffffffp-55, 0x1p-1074, -0x1p-1074})
+      t.add(split_exp(x), std::exp(x), x, 0);
+    fail |= t.report();
+  }
+  {  // pow with y*log(x) tiny (x next to 1, small y)
+    Tally t{"pow tiny y*log(x)"};
+    for (long long s = 0; s < M; ++s) {
+      const double x = 1.0 + (u01(rng) - 0.5) * std::exp2(-30.0 * u01(rng) - 20.0);
+      const double y = ((s & 1) ? -1.0 : 1.0) * std::exp2(-60.0 * u01(rng));
+      t.add(split_pow(x, y), std::pow(x, y), x, y);
+    }
+    fail |= t.report();
+  }
   {  // tiny and special arguments
     Tally t{"exp special"};
     const double xs[] = {0.0, -0.0, 1e-300, -1e-300, 0x1p-60, 709.78, 709.79, -708.4, -745.13, -745.14, 1e4, -1e4,
