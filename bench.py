@@ -41,8 +41,8 @@ def parse():
                         "(profiles/r01/nproma_sweep_all_variants.jsonl)")
     p.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
     p.add_argument("--variant", choices=["kseg", "kcache", "scc", "scc-private"], default=None,
-                   help="default: kseg for fp64 (2 waves/SIMD leave a tail the persistent kernel removes), "
-                        "kcache for fp32 (measured faster than kseg in fp32: profiles/r02/fp32_cfg_sweep.jsonl)")
+                   help="default: kseg (the persistent kernel: 2560 wave-sized units on 2 waves/SIMD without a "
+                        "tail; fp64 and fp32, profiles/r02/kseg_grid_sweep.jsonl)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--transfer", action="store_true",
                    help="also time the host-buffer path (H2D -> kernel -> D2H, chunked over streams): "
@@ -55,7 +55,7 @@ def parse():
                    help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     a = p.parse_args()
     if a.variant is None:
-        a.variant = "kseg" if a.precision == "fp64" else "kcache"
+        a.variant = "kseg"
     return a
 
 

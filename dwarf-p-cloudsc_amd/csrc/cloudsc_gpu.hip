@@ -323,11 +323,17 @@ namespace {
 
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
+  const int nseg = pa.nseg;
   auto kern = kseg_entry<real, WAVES, PF, AER, LDSC>;
   const int wg = kseg_wg(nproma);
   const size_t lds = LDSC ? carry_lds_bytes<real>(wg) : 0;
-  // one workgroup per resident slot (an over-estimate only delays the extra
-  // workgroups: progress never depends on residency, items are dequeued in order).
+  // Waves per SIMD: as many as fit, but no more than whole rounds of the work
+  // units (one column's 64-column sub-block) per SIMD: 2560 units on 1024 SIMDs
+  // take 2 waves each; a third resident wave (fp32 fits 3) would only find a
+  // next-segment item and spin until its predecessor finishes (fp32 KSEG 1.12 ms
+  // at 2 waves/SIMD against 1.23 ms at 3, profiles/r02/kseg_grid_sweep.jsonl).
+  // An over-estimate of residency only delays the extra workgroups: progress
+  // never depends on it, items are dequeued in order.
   // Cached per workgroup size; threads driving different devices may race here, hence atomics.
   static std::atomic<int> cache[65];
   int per_cu = cache[wg].load(std::memory_order_relaxed);
@@ -341,7 +347,13 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
     ncu = 256;
-  int grid = per_cu * ncu;
+  const int simds = 4 * ncu;
+  const int units = nitems / (nseg > 0 ? nseg : 1);
+  int per_simd = per_cu / 4 > 0 ? per_cu / 4 : 1;
+  int w = units / simds;
+  if (w < 1) w = 1;
+  if (w > per_simd) w = per_simd;
+  int grid = per_cu < 4 ? per_cu * ncu : w * simds;
   if (const int g = g_kseg_grid.load(std::memory_order_relaxed)) grid = g;
 #ifdef CLOUDSC_DEBUG_KNOBS
   grid = env_int("CLOUDSC_KSEG_GRID", 0) > 0 ? env_int("CLOUDSC_KSEG_GRID", 0) : grid;
