@@ -347,13 +347,14 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
     ncu = 256;
-  const int simds = 4 * ncu;
-  const int units = nitems / (nseg > 0 ? nseg : 1);
-  int per_simd = per_cu / 4 > 0 ? per_cu / 4 : 1;
+  constexpr int kSimdsPerCu = 4;                       // CDNA4 compute unit
+  const int simds = kSimdsPerCu * ncu;
+  const int units = nitems / (nseg > 0 ? nseg : 1);   // 64-column sub-blocks
+  const int per_simd = per_cu / kSimdsPerCu > 0 ? per_cu / kSimdsPerCu : 1;
   int w = units / simds;
   if (w < 1) w = 1;
   if (w > per_simd) w = per_simd;
-  int grid = per_cu < 4 ? per_cu * ncu : w * simds;
+  int grid = per_cu < kSimdsPerCu ? per_cu * ncu : w * simds;
   if (const int g = g_kseg_grid.load(std::memory_order_relaxed)) grid = g;
 #ifdef CLOUDSC_DEBUG_KNOBS
   grid = env_int("CLOUDSC_KSEG_GRID", 0) > 0 ? env_int("CLOUDSC_KSEG_GRID", 0) : grid;
