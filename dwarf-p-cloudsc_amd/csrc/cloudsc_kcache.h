@@ -278,8 +278,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     zfoeew = fmin(R(0.5), zfoeew);
     const Recip<real> r_iced = cl_recip(R(1.0) - c.retv * zfoeew);
     const real zqsice = cl_div(zfoeew, r_iced);
-    const real zfoeeliqt = fmin(cl_div((c.r2es * e_liq), r_pap), R(0.5));
-    const real zqsliq = cl_div(zfoeeliqt, (R(1.0) - c.retv * zfoeeliqt));
+    // (zqsliq, :601-604, is computed where rain evaporation, its only reader, runs)
     // liquid/ice fractions (:628-636)
     const real zli = zqx[QL] + zqx[QI];
     real zliqfrac = R(0.0), zicefrac = R(0.0);
@@ -669,13 +668,20 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
     }
 
-    // 4.5 evaporation of rain, Abel and Boutle (:1982-2040)
-    const real zzrh0 = fmin(fmax(c.rprecrhmax + cl_div(((R(1.0) - c.rprecrhmax) * cs.zcovpmax), r_1mza),
-                                 c.rprecrhmax), R(1.0));
-    {
-      const real zzrh = fmin(R(0.8), zzrh0);
+    // 4.5 evaporation of rain, Abel and Boutle (:1982-2040).  The humidity
+    // threshold zzrh0, zqsliq and zqe are pure functions of values fixed by now
+    // (cs.zcovpmax is not changed by either evaporation): they are evaluated
+    // inside the precipitation tests that guard their only uses, so a wave
+    // without rain or snow skips their divisions.  Same operations, same bits.
+    auto zzrh0_of = [&]() {
+      return fmin(fmax(c.rprecrhmax + cl_div(((R(1.0) - c.rprecrhmax) * cs.zcovpmax), r_1mza), c.rprecrhmax), R(1.0));
+    };
+    if (zcovpclr > zepsec && zqxfg[QR] > zepsec) {
+      const real zfoeeliqt = fmin(cl_div((c.r2es * e_liq), r_pap), R(0.5));
+      const real zqsliq = cl_div(zfoeeliqt, (R(1.0) - c.retv * zfoeeliqt));
+      const real zzrh = fmin(R(0.8), zzrh0_of());
       const real zqe = fmax(R(0.0), fmin(zqx[QV], zqsliq));
-      if (zcovpclr > zepsec && zqxfg[QR] > zepsec && zqe < zzrh * zqsliq) {
+      if (zqe < zzrh * zqsliq) {
         const real zpreclr = cl_div(zqxfg[QR], cs.zcovptot);
         const real zfallcorr = cl_pow<real>(cl_div(c.rdensref, zrho), R(0.4));
         const real zesatliq = c.rv_rd * (c.r2es * e_liq);
@@ -694,11 +700,11 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
     }
     // 4.5 evaporation of snow, Sundqvist (:2048-2087)
-    {
-      const real zzrh = zzrh0;
+    if (zcovpclr > zepsec && zqxfg[QS] > zepsec) {
+      const real zzrh = zzrh0_of();
       real zqe = cl_div((zqx[QV] - za * zqsice), r_1mza);
       zqe = fmax(R(0.0), fmin(zqe, zqsice));
-      if (zcovpclr > zepsec && zqxfg[QS] > zepsec && zqe < zzrh * zqsice) {
+      if (zqe < zzrh * zqsice) {
         const real x = cs.zcovptot * zdtgdp;
         const real zpreclr = cl_div((zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
         const real zbeta1 = cl_div(((cl_div(sqrt(cl_div(pap_k, cc.paph_sfc)), c.rvrfactor)) * zpreclr), fmax(zcovpclr, zepsec));
