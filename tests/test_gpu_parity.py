@@ -315,15 +315,16 @@ def test_random_perturbations_vs_oracle(lib, ds, oracle_mod, seed, variant):
 
 
 @pytest.mark.parametrize("nssopt", [0, 2, 3])
-def test_nssopt_vs_oracle(lib, ds, oracle_mod, nssopt):
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_SCC_PRIVATE])
+def test_nssopt_vs_oracle(lib, ds, oracle_mod, nssopt, variant):
     s = ds.copy()
     s.params["nssopt"] = nssopt
-    out = run_gpu(s, 300, 128)
+    out = run_gpu(s, 300, 128, variant=variant)
     ref = oracle_outputs(oracle_mod, s, 300, 128)
     assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "nssopt %d" % nssopt)
 
 
-@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE])
 def test_aerosol_flags_vs_oracle(lib, ds, oracle_mod, variant):
     import make_fixtures as mf
     s = mf.with_aerosols(ds)
@@ -401,7 +402,7 @@ def sliced_levels(ds, lo_lev):
     return s
 
 
-@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE])
 def test_other_klev_vs_oracle(lib, ds, oracle_mod, variant):
     s = sliced_levels(ds, 77)                          # KLEV = 60
     out = run_gpu(s, 300, 64, variant=variant)
@@ -410,7 +411,7 @@ def test_other_klev_vs_oracle(lib, ds, oracle_mod, variant):
 
 
 @pytest.mark.parametrize("ngptot,nproma", [(1, 1), (1, 64), (5, 256), (127, 64), (257, 256), (64, 32)])
-@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC_PRIVATE])
 def test_tiny_and_ragged(lib, ds, oracle_mod, ngptot, nproma, variant):
     out = run_gpu(ds, ngptot, nproma, variant=variant)
     ref = oracle_outputs(oracle_mod, ds, ngptot, nproma)
