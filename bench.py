@@ -34,7 +34,9 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)    # 0.2 s of kernels: a stable mean
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=20,
+                   help="untimed steps; the board settles its shader clock over the first ~10-15 launches of the "
+                        "fp64 kernel (profiles/r02/clock_probe_bench_run.json)")
     p.add_argument("--ngptot", type=int, default=163840, help="columns per GPU")
     p.add_argument("--nproma", type=int, default=64,
                    help="NPROMA (block = workgroup); 64 is the measured best for the persistent kernel "
