@@ -491,7 +491,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       real zrhc = c.ramid;
       const real zsigk = cl_div(pap_k, cc.paph_sfc);
       if (zsigk > R(0.8)) {
-        const real s = cl_div((zsigk - R(0.8)), R(0.2));
+        const real s = cl_div_lit((zsigk - R(0.8)), R(0.2));
         zrhc = c.ramid + (R(1.0) - c.ramid) * (s * s);
       }
       real zqe = R(0.0);
@@ -530,7 +530,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
     else cs.zcldtopdist = cs.zcldtopdist + cl_div(zdp, (zrho * c.rg));
     if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
-      const real zvpice = cl_div(((c.r2es * e_ice) * c.rv), c.rd);
+      const real zvpice = cl_div_known(((c.r2es * e_ice) * c.rv), c.rd, c.rd_rcp);
       const real zvpliq = zvpice * zfokoop;
       const real zicenuclei = R(1000.0) * cl_exp<real>(cl_div((R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
       const real zadd = cl_div((c.rlstt * (cl_div(c.rlstt, (c.rv * ztp1)) - R(1.0))), (R(0.024) * ztp1));
@@ -540,8 +540,8 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       const real zinew = cl_pow<real>((R(0.666) * zcvds) * c.ptsphy + cl_pow<real>(zice0, R(0.666)), R(1.5));
       real zdepos = fmax(za * (zinew - zice0), R(0.0));
       zdepos = fmin(zdepos, zqxfg[QL]);
-      const real zinfactor = fmin(cl_div(zicenuclei, R(15000.0)), R(1.0));
-      zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cl_div(cs.zcldtopdist, c.rdepliqrefdepth)), R(1.0));
+      const real zinfactor = fmin(cl_div_lit(zicenuclei, R(15000.0)), R(1.0));
+      zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cl_div_known(cs.zcldtopdist, c.rdepliqrefdepth, c.rdepliqrefdepth_rcp)), R(1.0));
       sa_li = sa_li + zdepos;
       zqxfg[QI] = zqxfg[QI] + zdepos; zqxfg[QL] = zqxfg[QL] - zdepos;
     }
@@ -619,7 +619,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (zicetot > zepsec && ztp1 > c.rtt) {
       const real zsubsat = fmax(zqsice - zqx[QV], R(0.0));
       const real ztdmtw0 = ztp1 - c.rtt - zsubsat * (ztw1 + ztw2 * (pap_k - ztw3) - ztw4 * (ztp1 - ztw5));
-      const real zcons1 = fabs(cl_div((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)), c.rtaumel));
+      const real zcons1 = fabs(cl_div_known((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)), c.rtaumel, c.rtaumel_rcp));
       const real zmeltmax = fmax((ztdmtw0 * zcons1) * c.zrldcp, R(0.0));
       if (zmeltmax > zepsec) {
         {   // ice -> rain
@@ -651,7 +651,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
           const real zfrz = ((c.ptsphy * (cl_div(c.rcl_const5r, zrho))) * (cl_exp<real>(ztemp) - R(1.0))) * cl_pow<real>(zlambda, c.rcl_const6r);
           zfrzmax = fmax(zfrz, R(0.0));
         } else {
-          const real zcons1 = fabs(cl_div((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))), c.rtaumel));
+          const real zcons1 = fabs(cl_div_known((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))), c.rtaumel, c.rtaumel_rcp));
           zfrzmax = fmax(((c.rtt - ztp1) * zcons1) * c.zrldcp, R(0.0));
         }
         if (zfrzmax > zepsec) {
@@ -687,7 +687,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
         const real zesatliq = c.rv_rd * (c.r2es * e_liq);
         const real zlambda = cl_pow<real>(cl_div(c.rcl_fac1, (zrho * zpreclr)), c.rcl_fac2);
         const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * cl_pow<real>(ztp1, R(3.0))) * pap_k;
-        const real zcorr2 = cl_div((cl_pow<real>(cl_div(ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
+        const real zcorr2 = cl_div((cl_pow<real>(cl_div_lit(ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
         const real zsubsat = fmax(zzrh * zqsliq - zqe, R(0.0));
         const real zbeta = ((((cl_div(R(0.5), zqsliq)) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (cl_div(zcorr2, zevap_denom)) *
                            (cl_div(R(0.78), cl_pow<real>(zlambda, c.rcl_const4r)) + cl_div((c.rcl_const2r * sqrt(zrho * zfallcorr)), (sqrt(zcorr2) * cl_pow<real>(zlambda, c.rcl_const3r))));
@@ -707,7 +707,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       if (zqe < zzrh * zqsice) {
         const real x = cs.zcovptot * zdtgdp;
         const real zpreclr = cl_div((zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
-        const real zbeta1 = cl_div(((cl_div(sqrt(cl_div(pap_k, cc.paph_sfc)), c.rvrfactor)) * zpreclr), fmax(zcovpclr, zepsec));
+        const real zbeta1 = cl_div(((cl_div_known(sqrt(cl_div(pap_k, cc.paph_sfc)), c.rvrfactor, c.rvrfactor_rcp)) * zpreclr), fmax(zcovpclr, zepsec));
         const real zbeta = c.rg_rpecons * cl_pow<real>(zbeta1, R(0.5777));
         const real zdenom = R(1.0) + (zbeta * c.ptsphy) * zcorqsice;
         const real zdpr = ((cl_div(((zcovpclr * zbeta) * (zqsice - zqe)), zdenom)) * zdp) * c.zrg_r;

@@ -44,6 +44,10 @@ inline DevParams<real> fold_params(const cloudsc_params_t& p) {
   d.rv_rd = (real)p.rv / rd;
   d.rg_rpecons = rg * (real)p.rpecons;
   d.one_m_ramin = one - (real)p.ramin;
+  d.rd_rcp = one / rd;
+  d.rtaumel_rcp = one / (real)p.rtaumel;
+  d.rdepliqrefdepth_rcp = one / (real)p.rdepliqrefdepth;
+  d.rvrfactor_rcp = one / (real)p.rvrfactor;
   d.nssopt = p.nssopt;
   d.ncldtop = p.ncldtop;
   d.laericesed = p.laericesed;

@@ -58,3 +58,18 @@ def test_tables_are_generated(tmp_path):
         assert "0x%016xULL, 0x%016xULL" % (t, s) in text
     for invc, logc, tail in log_rows:
         assert "%s, %s, %s, 0.0" % (invc.hex(), logc.hex(), tail.hex()) in text
+
+
+def test_known_divisor_division(tmp_path):
+    """cl_div_known / cl_div_lit (cloudsc_dev.h): with the host's r = RN(1/d)
+    the one-correction quotient (two in fp32) is the IEEE n/d, for CLOUDSC's
+    constant divisors and random ones (tools/div_const_check.c)."""
+    cc = shutil.which("gcc")
+    if cc is None:
+        pytest.skip("no gcc")
+    exe = str(tmp_path / "div_const_check")
+    subprocess.check_call([cc, "-O2", "-ffp-contract=off", os.path.join(REPO, "tools", "div_const_check.c"),
+                           "-lm", "-o", exe])
+    r = subprocess.run([exe, "2"], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0 and "total mismatches 0" in r.stdout, r.stdout + r.stderr
