@@ -525,12 +525,18 @@ def test_bitwise_random_perturbations(lib, ds, oracle_mod, seed):
     assert bitwise_mismatches(out, ref) == {}
 
 
-@pytest.mark.parametrize("case", ["nssopt0", "nssopt2", "nssopt3", "aerosol", "klev60"])
+@pytest.mark.parametrize("case", ["nssopt0", "nssopt2", "nssopt3", "aerosol", "klev60", "divisor_params"])
 def test_bitwise_other_configurations(lib, ds, oracle_mod, case):
     import make_fixtures as mf
     if case.startswith("nssopt"):
         s = ds.copy()
         s.params["nssopt"] = int(case[-1])
+    elif case == "divisor_params":
+        # the parameters the kernel divides by through host-folded reciprocals
+        # (cl_div_known): other values with full mantissas, still the oracle's n/d
+        s = ds.copy()
+        for name, f in (("rtaumel", 0.7310432), ("rdepliqrefdepth", 1.913), ("rvrfactor", 1.3370001), ("rd", 1.0000137)):
+            s.params[name] = s.params[name] * f
     elif case == "aerosol":
         s = mf.with_aerosols(ds)
     else:
