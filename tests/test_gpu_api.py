@@ -185,13 +185,14 @@ def test_bitwise_scc_private_full_size(lib, ds):
 
 def test_bitwise_fp32_full_size(lib, ds, oracle_mod):
     """BASELINE.json config 4: SCC-k-caching fp32, NGPTOT 163840 (NPROMA 64, the
-    fp32 bench default) -- bit-equal to the fp32 restatement at the same size;
+    fp32 bench default) -- KCACHE, KSEG and both SCC forms bit-equal to the fp32
+    restatement at the same size;
     per-field relL1 vs reference.h5 (fp64) printed, and no worse than 2x the fp32
     CPU restatement's own (SURVEY.md §8c gate; fp32 is parity-unpinned beyond the
     restatement: the reference has no fp32 C kernel)."""
     n = 163840
     out = {}
-    for variant in (ca.VARIANT_KCACHE, ca.VARIANT_KSEG):
+    for variant in (ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE):
         g = ca.GpuState(ds, n, 64, ca.FP32)
         try:
             out[variant] = outputs_of(g, variant)
