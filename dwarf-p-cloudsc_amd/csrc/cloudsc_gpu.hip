@@ -306,9 +306,11 @@ std::atomic<int> g_kseg_nseg{0}, g_kseg_grid{0};
 
 // KSEG workspace words: [0] dequeue counter, [1] timed-out hand-offs (sticky:
 // accumulated over launches until cloudsc_gpu_check reads and clears it),
-// [2] a tag marking [1] as initialised, [64..] per-sub-block flags.  Every
-// launch zeroes the counter and the flags; the first launch on a workspace
-// (tag absent) also zeroes the error word.
+// [2] a tag marking [1] as initialised, [64..] per-sub-block flags.  This
+// kernel zeroes the counter and the flags before every launch of the low-level
+// entry points, and before the first launch on a state's workspace (later
+// launches of the state continue the counter and the flag stamps, KsegEpoch);
+// the first launch on a workspace (tag absent) also zeroes the error word.
 constexpr unsigned kKsegTag = 0xC105D5C1u;
 __global__ void __launch_bounds__(256) kseg_prepare_kernel(unsigned* ws, int nflags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -322,7 +324,8 @@ __global__ void __launch_bounds__(256) kseg_prepare_kernel(unsigned* ws, int nfl
 namespace {
 
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
-int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
+int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
+                    int* grid_out) {
   const int nseg = pa.nseg;
   auto kern = kseg_entry<real, WAVES, PF, AER, LDSC>;
   const int wg = kseg_wg(nproma);
@@ -361,27 +364,30 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
 #endif
   if (grid > nitems) grid = nitems;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, st, a, pa);
+  *grid_out = grid;
   return CLOUDSC_OK;
 }
 
 template <typename real, bool AER>
-int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems) {
+int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
+                int* grid_out) {
 #ifdef CLOUDSC_DEBUG_KNOBS
   switch (env_int("CLOUDSC_KCACHE_CFG", DefaultCfg<real>::code)) {
 #define X(code, w, pf, ldsc) \
-  case code: return launch_kseg_cfg<real, w, pf, AER, ldsc>(st, a, pa, nproma, nitems);
+  case code: return launch_kseg_cfg<real, w, pf, AER, ldsc>(st, a, pa, nproma, nitems, grid_out);
     CLOUDSC_FOR_EACH_CFG(X)
 #undef X
     default: return CLOUDSC_EINVAL;
   }
 #else
-  return launch_kseg_cfg<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>(st, a, pa, nproma, nitems);
+  return launch_kseg_cfg<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>(st, a, pa, nproma, nitems,
+                                                                                        grid_out);
 #endif
 }
 
 template <typename real>
 int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
-           void* scratch, const void* plude_in, const ParamSet& ps) {
+           void* scratch, const void* plude_in, const ParamSet& ps, KsegEpoch* ep) {
   KArgs<real> a = make_args<real>(f, ngptot, nproma, klev, ps);
   if (plude_in) a.plude_in = (const real*)plude_in;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
@@ -428,12 +434,25 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
     }
 #endif
     pa.nitems = pa.nseg * nblocks * pa.nsub;
-    {
+    const bool zero_ws = !(ep && ep->ready);
+    if (zero_ws) {
       const int nflags = nblocks * pa.nsub;
       const int g = (nflags + 255) / 256 < 64 ? (nflags + 255) / 256 : 64;
       hipLaunchKernelGGL(kseg_prepare_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, (unsigned*)scratch, nflags);
+      if (ep) ep->ready = false;
     }
-    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems) : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems);
+    pa.base = zero_ws ? 0u : ep->base;
+    pa.stamp = zero_ws ? 0u : ep->stamp;
+    int grid = 0;
+    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, &grid)
+             : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, &grid);
+    if (rc) return rc;
+    HIPCHK(hipGetLastError());
+    if (ep) {   // the next launch on this workspace continues where this one ends
+      ep->base = pa.base + (unsigned)pa.nitems + (unsigned)grid;
+      ep->stamp = pa.stamp + (unsigned)(kMaxSeg + 1);
+      ep->ready = true;
+    }
   } else if (variant == CLOUDSC_VARIANT_SCC_PRIVATE) {
     if (klev > kPrivKlev) return CLOUDSC_EINVAL;    // the private arrays are sized at compile time
     if (aer) hipLaunchKernelGGL((scc_private_entry<real, true>), dim3(nblocks), dim3(nproma), 0, st, a);
@@ -514,7 +533,8 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
 // values of plude are read from there and the results written to f->plude.
 // ps: the parameter set of the launch (NULL = the device's default set).
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
-                 const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps) {
+                 const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps,
+                 KsegEpoch* ep) {
   int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
   if (rc) return rc;
   if (!ps) ps = device_default_params(device);
@@ -523,8 +543,8 @@ int gpu_run_impl(int device, void* stream, int precision, int variant, int ngpto
   if (!f || !fields_complete(f)) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
-  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps)
-                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps);
+  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep)
+                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep);
 }
 
 int kseg_check(int device, void* stream, void* scratch) {

@@ -36,10 +36,19 @@ void set_error_text(const char* text);
 int validate_run_args(int device, int precision, int variant, int ngptot, int nproma, int klev);
 // every pointer the kernel reads or writes (aerosol inputs excepted) is set
 bool fields_complete(const cloudsc_fields_t* f);
-// cloudsc_gpu_run with an optional separate source of plude (NULL = in place)
-// and an explicit parameter set (NULL = the device's default set)
+// Host record of one KSEG workspace owned by a caller that launches on it in
+// stream order (a state): after the first launch zeroes it, later launches
+// continue its ticket counter and flag stamps instead of zeroing it again.
+struct KsegEpoch {
+  bool ready = false;       // false: zero the workspace before the next launch
+  unsigned base = 0, stamp = 0;
+};
+// cloudsc_gpu_run with an optional separate source of plude (NULL = in place),
+// an explicit parameter set (NULL = the device's default set) and an optional
+// KSEG workspace record (NULL = zero the workspace before every KSEG launch)
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
-                 const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps);
+                 const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps,
+                 KsegEpoch* ep = nullptr);
 // waits for `stream` and returns CLOUDSC_EHANDOFF if the last KSEG launch on
 // `scratch` counted a timed-out segment hand-off
 int kseg_check(int device, void* stream, void* scratch);

@@ -1093,9 +1093,15 @@ __device__ unsigned long long g_kseg_trace[4 * kTraceMax];
 
 template <typename real>
 struct PersistArgs {
-  unsigned* counter;      // dequeue counter (zeroed per launch)
-  unsigned* flags;        // [nblocks * nsub] segments completed (zeroed per launch)
-  unsigned* err;          // spin-limit violations (zeroed per launch)
+  // The workspace is zeroed before the first launch on it; later launches on
+  // the same workspace (a state's steps) need no zeroing: each launch takes
+  // exactly nitems + grid tickets, so the host passes the counter's value at
+  // its start (base), and flags are stamped per launch (stamp + segments done;
+  // an older launch's flag compares as "not yet": signed difference).
+  unsigned* counter;      // dequeue counter: this launch's tickets are base, base + 1, ...
+  unsigned* flags;        // [nblocks * nsub] stamp + segments completed
+  unsigned* err;          // spin-limit violations (sticky until read, cloudsc_gpu_check)
+  unsigned base, stamp;   // 0, 0 right after zeroing
   real* state;            // [nblocks][kCarryN][nproma]
   int nseg, nitems, nblocks;
   int nsub;               // 64-column sub-blocks per NPROMA block (one wave each)
@@ -1148,7 +1154,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
   for (;;) {
     if (wave0) {
       const unsigned old = __hip_atomic_fetch_add(P.counter, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_item = (int)__builtin_amdgcn_readfirstlane(old);   // lane 0's value: the ticket
+      s_item = (int)(__builtin_amdgcn_readfirstlane(old) - P.base);   // lane 0's value: the ticket
     }
     __syncthreads();
     const int item = __builtin_amdgcn_readfirstlane(s_item);
@@ -1187,7 +1193,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
           }
           const unsigned f = __builtin_amdgcn_readfirstlane(
               __hip_atomic_load(P.flags + sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          if (f >= (unsigned)seg) break;
+          if ((int)(f - (P.stamp + (unsigned)seg)) >= 0) break;
           __builtin_amdgcn_s_sleep(4);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1206,7 +1212,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, true);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (wave0) __hip_atomic_store(P.flags + sb, (unsigned)(seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (wave0) __hip_atomic_store(P.flags + sb, P.stamp + (unsigned)(seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (active) {
       stg(((const KArgs<real>*)launder_uniform(ka))->prainfrac, (size_t)b * nproma, lo, cs.rainfrac);
     }

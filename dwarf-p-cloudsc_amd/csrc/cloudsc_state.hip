@@ -75,6 +75,7 @@ struct cloudsc_gpu_state {
   void* plude_pristine;
   void* scratch;                  // SCC temporaries
   void* kseg_ws;                  // KSEG counter, flags and carried state
+  cloudsc_impl::KsegEpoch kseg_epoch;   // where the last launch on kseg_ws left its counter and flag stamps
   ParamSet params;                // the state's own parameter set (never shared)
   std::vector<void*> allocs;
 };
@@ -251,7 +252,7 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     // result to f.plude, so repeated steps see the same input with no restore copy
     HIPCHK(hipEventRecord(ev[2 * r], s->stream));
     rc = gpu_run_impl(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f, scratch,
-                      s->plude_pristine, &s->params);
+                      s->plude_pristine, &s->params, &s->kseg_epoch);
     HIPCHK(hipEventRecord(ev[2 * r + 1], s->stream));
   }
   hipError_t e = hipStreamSynchronize(s->stream);
@@ -270,6 +271,7 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     // every later step too, so the last step's count is the one to read.
     rc = kseg_check(s->device, s->stream, scratch);
   }
+  if (rc != CLOUDSC_OK) s->kseg_epoch.ready = false;   // zero the workspace again before the next launch
   return rc;
 }
 

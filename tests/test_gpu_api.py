@@ -214,3 +214,32 @@ def test_bitwise_fp32_full_size(lib, ds, oracle_mod):
     for k in g_rep:
         print("fp32 @163840 vs reference.h5 %-18s relL1 gpu %.3e cpu %.3e" % (k, g_rep[k][0], c_rep[k][0]))
         assert g_rep[k][0] <= 2.0 * c_rep[k][0] + 1e-6, k
+
+
+def test_kseg_consecutive_launches_on_one_workspace(lib, ds):
+    """A state zeroes its KSEG workspace once; later launches continue the
+    ticket counter and the flag stamps (KsegEpoch, cloudsc_gpu.hip).  Many
+    launches in one call, calls in a row, a schedule change (segments, grid)
+    between calls, and a hand-off timeout (which makes the next call zero the
+    workspace again): every result is bit-equal to KCACHE on the same state."""
+    n = 20000
+    g = ca.GpuState(ds, n, 64)
+    try:
+        ref = outputs_of(g, ca.VARIANT_KCACHE)
+        assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=7), ref) == {}
+        assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=2), ref) == {}
+        for nseg, grid in ((4, 0), (3, 97), (1, 0), (0, 0)):
+            ca.kseg_schedule(nseg, grid)
+            try:
+                assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=3), ref) == {}, (nseg, grid)
+            finally:
+                ca.kseg_schedule(0, 0)
+        ca.kseg_spin_limit(0)
+        try:
+            with pytest.raises(ca.CloudscError):
+                g.run(ca.VARIANT_KSEG, 2)
+        finally:
+            ca.kseg_spin_limit(-1)
+        assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=3), ref) == {}
+    finally:
+        g.close()
