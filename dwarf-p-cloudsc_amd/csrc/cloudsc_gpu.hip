@@ -16,6 +16,7 @@
 // the device is unavailable.  (cloudsc_cpu_run, cloudsc_cpu.cpp, is a separate,
 // explicitly selected host variant, never substituted for a GPU run.)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <atomic>
 #include <cstdio>
@@ -236,22 +237,32 @@ int env_int(const char* name, int dflt) {
 }
 #endif
 
+// One physics-kernel launch.  With `ev`, the dispatch packet itself records the
+// start and stop timestamps (hipExtLaunchKernelGGL), so timing a step adds no
+// event packets between consecutive kernels.
+template <typename... Args>
+void launch_physics(void (*kern)(Args...), dim3 grid, dim3 block, size_t lds, hipStream_t st, const LaunchEvents* ev,
+                    Args... args) {
+  if (ev) hipExtLaunchKernelGGL(kern, grid, block, (std::uint32_t)lds, st, ev->start, ev->stop, 0u, args...);
+  else hipLaunchKernelGGL(kern, grid, block, lds, st, args...);
+}
+
 template <typename real, bool AER>
-int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma) {
+int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma, const LaunchEvents* ev) {
 #ifdef CLOUDSC_DEBUG_KNOBS
   switch (env_int("CLOUDSC_KCACHE_CFG", DefaultCfg<real>::code)) {
 #define X(code, w, pf, ldsc)                                                                                 \
   case code:                                                                                                 \
-    hipLaunchKernelGGL((kcache_entry<real, w, pf, AER, ldsc>), dim3(nblocks), dim3(nproma),                  \
-                       ldsc ? carry_lds_bytes<real>(nproma) : 0, st, a);                                     \
+    launch_physics(kcache_entry<real, w, pf, AER, ldsc>, dim3(nblocks), dim3(nproma),                       \
+                   ldsc ? carry_lds_bytes<real>(nproma) : 0, st, ev, a);                                     \
     return CLOUDSC_OK;
     CLOUDSC_FOR_EACH_CFG(X)
 #undef X
     default: return CLOUDSC_EINVAL;
   }
 #else
-  hipLaunchKernelGGL((kcache_entry<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>), dim3(nblocks),
-                     dim3(nproma), 0, st, a);
+  launch_physics(kcache_entry<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>, dim3(nblocks),
+                 dim3(nproma), 0, st, ev, a);
   return CLOUDSC_OK;
 #endif
 }
@@ -325,7 +336,7 @@ namespace {
 
 template <typename real, int WAVES, int PF, bool AER, bool LDSC>
 int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
-                    int* grid_out) {
+                    int* grid_out, const LaunchEvents* ev) {
   const int nseg = pa.nseg;
   auto kern = kseg_entry<real, WAVES, PF, AER, LDSC>;
   const int wg = kseg_wg(nproma);
@@ -363,31 +374,31 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   grid = env_int("CLOUDSC_KSEG_GRID", 0) > 0 ? env_int("CLOUDSC_KSEG_GRID", 0) : grid;
 #endif
   if (grid > nitems) grid = nitems;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, st, a, pa);
+  launch_physics(kern, dim3(grid), dim3(wg), lds, st, ev, a, pa);
   *grid_out = grid;
   return CLOUDSC_OK;
 }
 
 template <typename real, bool AER>
 int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
-                int* grid_out) {
+                int* grid_out, const LaunchEvents* ev) {
 #ifdef CLOUDSC_DEBUG_KNOBS
   switch (env_int("CLOUDSC_KCACHE_CFG", DefaultCfg<real>::code)) {
 #define X(code, w, pf, ldsc) \
-  case code: return launch_kseg_cfg<real, w, pf, AER, ldsc>(st, a, pa, nproma, nitems, grid_out);
+  case code: return launch_kseg_cfg<real, w, pf, AER, ldsc>(st, a, pa, nproma, nitems, grid_out, ev);
     CLOUDSC_FOR_EACH_CFG(X)
 #undef X
     default: return CLOUDSC_EINVAL;
   }
 #else
   return launch_kseg_cfg<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>(st, a, pa, nproma, nitems,
-                                                                                        grid_out);
+                                                                                        grid_out, ev);
 #endif
 }
 
 template <typename real>
 int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
-           void* scratch, const void* plude_in, const ParamSet& ps, KsegEpoch* ep) {
+           void* scratch, const void* plude_in, const ParamSet& ps, KsegEpoch* ep, const LaunchEvents* ev) {
   KArgs<real> a = make_args<real>(f, ngptot, nproma, klev, ps);
   if (plude_in) a.plude_in = (const real*)plude_in;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
@@ -395,7 +406,7 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
   if (aer && (!f->pre_ice || !f->picrit_aer || !f->pnice)) return CLOUDSC_EINVAL;
   int rc = CLOUDSC_OK;
   if (variant == CLOUDSC_VARIANT_KCACHE) {
-    rc = aer ? launch_kcache<real, true>(st, a, nblocks, nproma) : launch_kcache<real, false>(st, a, nblocks, nproma);
+    rc = aer ? launch_kcache<real, true>(st, a, nblocks, nproma, ev) : launch_kcache<real, false>(st, a, nblocks, nproma, ev);
   } else if (variant == CLOUDSC_VARIANT_KSEG) {
     if (!scratch) return CLOUDSC_EINVAL;
     PersistArgs<real> pa;
@@ -444,8 +455,8 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
     pa.base = zero_ws ? 0u : ep->base;
     pa.stamp = zero_ws ? 0u : ep->stamp;
     int grid = 0;
-    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, &grid)
-             : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, &grid);
+    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, &grid, ev)
+             : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, &grid, ev);
     if (rc) return rc;
     HIPCHK(hipGetLastError());
     if (ep) {   // the next launch on this workspace continues where this one ends
@@ -455,13 +466,13 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
     }
   } else if (variant == CLOUDSC_VARIANT_SCC_PRIVATE) {
     if (klev > kPrivKlev) return CLOUDSC_EINVAL;    // the private arrays are sized at compile time
-    if (aer) hipLaunchKernelGGL((scc_private_entry<real, true>), dim3(nblocks), dim3(nproma), 0, st, a);
-    else hipLaunchKernelGGL((scc_private_entry<real, false>), dim3(nblocks), dim3(nproma), 0, st, a);
+    if (aer) launch_physics(scc_private_entry<real, true>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
+    else launch_physics(scc_private_entry<real, false>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
   } else {
     if (!scratch) return CLOUDSC_EINVAL;
     SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
-    if (aer) hipLaunchKernelGGL((scc_entry<real, true>), dim3(nblocks), dim3(nproma), 0, st, a, s);
-    else hipLaunchKernelGGL((scc_entry<real, false>), dim3(nblocks), dim3(nproma), 0, st, a, s);
+    if (aer) launch_physics(scc_entry<real, true>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
+    else launch_physics(scc_entry<real, false>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
   }
   if (rc) return rc;
   HIPCHK(hipGetLastError());
@@ -534,7 +545,7 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
 // ps: the parameter set of the launch (NULL = the device's default set).
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
                  const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps,
-                 KsegEpoch* ep) {
+                 KsegEpoch* ep, const LaunchEvents* lev) {
   int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
   if (rc) return rc;
   if (!ps) ps = device_default_params(device);
@@ -543,8 +554,8 @@ int gpu_run_impl(int device, void* stream, int precision, int variant, int ngpto
   if (!f || !fields_complete(f)) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
-  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep)
-                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep);
+  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev)
+                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev);
 }
 
 int kseg_check(int device, void* stream, void* scratch) {

@@ -43,12 +43,18 @@ struct KsegEpoch {
   bool ready = false;       // false: zero the workspace before the next launch
   unsigned base = 0, stamp = 0;
 };
+// Start/stop events of one launch, recorded by the kernel's own dispatch
+// (hipExtLaunchKernelGGL) instead of separate event packets around it.
+struct LaunchEvents {
+  hipEvent_t start, stop;
+};
 // cloudsc_gpu_run with an optional separate source of plude (NULL = in place),
-// an explicit parameter set (NULL = the device's default set) and an optional
+// an explicit parameter set (NULL = the device's default set), an optional
 // KSEG workspace record (NULL = zero the workspace before every KSEG launch)
+// and optional events timing the physics kernel (NULL = none)
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
                  const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps,
-                 KsegEpoch* ep = nullptr);
+                 KsegEpoch* ep = nullptr, const LaunchEvents* lev = nullptr);
 // waits for `stream` and returns CLOUDSC_EHANDOFF if the last KSEG launch on
 // `scratch` counted a timed-out segment hand-off
 int kseg_check(int device, void* stream, void* scratch);
