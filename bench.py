@@ -14,8 +14,9 @@ kernel launch reading every input (plude from the state's pristine copy: the
 INOUT field is taken out of place, so repeated steps are the same step) and
 writing every output.  The timed region brackets exactly K steps with barrier
 + device sync on both sides; value = all columns of all ranks / max-over-ranks
-wall time.  The kernel alone is also timed with HIP events recorded on the
-launch stream (roofline.achieved uses that kernel time).
+wall time.  The kernel alone is also timed with HIP start/stop events on the
+launch stream, recorded by the kernel's own dispatch packet
+(hipExtLaunchKernelGGL; roofline.achieved uses that kernel time).
 """
 import argparse
 import json
@@ -174,7 +175,7 @@ def main():
     g.sync()
     ctl.barrier()
     t0 = time.perf_counter()
-    kernel_ms = g.run(variant, args.steps)      # one launch per step; events around each launch
+    kernel_ms = g.run(variant, args.steps)      # one launch per step; its dispatch records its events
     g.sync()
     t1 = time.perf_counter()
     ctl.barrier()
