@@ -216,14 +216,15 @@ def test_bitwise_fp32_full_size(lib, ds, oracle_mod):
         assert g_rep[k][0] <= 2.0 * c_rep[k][0] + 1e-6, k
 
 
-def test_kseg_consecutive_launches_on_one_workspace(lib, ds):
+@pytest.mark.parametrize("nproma", [64, 128, 48])
+def test_kseg_consecutive_launches_on_one_workspace(lib, ds, nproma):
     """A state zeroes its KSEG workspace once; later launches continue the
     ticket counter and the flag stamps (KsegEpoch, cloudsc_gpu.hip).  Many
     launches in one call, calls in a row, a schedule change (segments, grid)
     between calls, and a hand-off timeout (which makes the next call zero the
     workspace again): every result is bit-equal to KCACHE on the same state."""
-    n = 20000
-    g = ca.GpuState(ds, n, 64)
+    n = 20000 if nproma != 48 else 20001     # ragged last block in every case
+    g = ca.GpuState(ds, n, nproma)
     try:
         ref = outputs_of(g, ca.VARIANT_KCACHE)
         assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=7), ref) == {}
