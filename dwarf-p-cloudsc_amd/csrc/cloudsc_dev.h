@@ -372,10 +372,15 @@ CLOUDSC_HD float cl_div(float n, const Recip<float>& rd) {
 // n/d correctly rounded (Markstein's theorem; tools/div_const_check.c: 0
 // mismatches over 1.4e8 numerators for CLOUDSC's divisors, and 1000 random
 // divisors, in fp64 and fp32).
+// (real is deduced from the divisor; the numerator converts, e.g. from an LDS-carried value)
 template <typename real>
-CLOUDSC_HD real cl_div_known(real n, real d, real rcp_d) { return cl_div(n, Recip<real>{d, rcp_d}); }
+CLOUDSC_HD real cl_div_known(typename std::common_type<real>::type n, real d, real rcp_d) {
+  return cl_div(n, Recip<real>{d, rcp_d});
+}
 template <typename real>
-CLOUDSC_HD real cl_div_lit(real n, real d) { return cl_div(n, Recip<real>{d, real(1) / d}); }
+CLOUDSC_HD real cl_div_lit(typename std::common_type<real>::type n, real d) {
+  return cl_div(n, Recip<real>{d, real(1) / d});
+}
 // explicit-precision form, cl_div<real>(a, b)
 template <typename real>
 CLOUDSC_HD real cl_div(typename std::common_type<real>::type n, typename std::common_type<real>::type d) {
