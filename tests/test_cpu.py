@@ -50,10 +50,13 @@ def test_cpu_run_scenarios_vs_reference_outputs(scenarios, name):
     assert bits_equal(cpu_outputs(s, 100, 32), s.reference) == {}
 
 
-@pytest.mark.parametrize("case", ["nssopt0", "nssopt3", "aerosol", "seed2"])
+@pytest.mark.parametrize("case", ["nssopt0", "nssopt3", "aerosol", "seed2", "ncldtop2", "ncldtop40", "ncldtop138"])
 def test_cpu_run_other_configurations(ds, oracle_mod, case):
     import make_fixtures as mf
-    if case.startswith("nssopt"):
+    if case.startswith("ncldtop"):
+        s = ds.copy()
+        s.params["ncldtop"] = int(case[len("ncldtop"):])
+    elif case.startswith("nssopt"):
         s = ds.copy()
         s.params["nssopt"] = int(case[-1])
     elif case == "aerosol":

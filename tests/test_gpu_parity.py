@@ -525,10 +525,15 @@ def test_bitwise_random_perturbations(lib, ds, oracle_mod, seed):
     assert bitwise_mismatches(out, ref) == {}
 
 
-@pytest.mark.parametrize("case", ["nssopt0", "nssopt2", "nssopt3", "aerosol", "klev60", "divisor_params"])
+@pytest.mark.parametrize("case", ["nssopt0", "nssopt2", "nssopt3", "aerosol", "klev60", "divisor_params",
+                                  "ncldtop2", "ncldtop40", "ncldtop120", "ncldtop137", "ncldtop138"])
 def test_bitwise_other_configurations(lib, ds, oracle_mod, case):
     import make_fixtures as mf
-    if case.startswith("nssopt"):
+    if case.startswith("ncldtop"):
+        # the physics starts at NCLDTOP; KSEG's segment bounds follow it (kseg_bounds)
+        s = ds.copy()
+        s.params["ncldtop"] = int(case[len("ncldtop"):])
+    elif case.startswith("nssopt"):
         s = ds.copy()
         s.params["nssopt"] = int(case[-1])
     elif case == "divisor_params":
@@ -541,9 +546,13 @@ def test_bitwise_other_configurations(lib, ds, oracle_mod, case):
         s = mf.with_aerosols(ds)
     else:
         s = sliced_levels(ds, 77)
-    out = run_gpu(s, 300, 64, variant=ca.VARIANT_KSEG)
     ref = oracle_outputs(oracle_mod, s, 300, 64)
-    assert bitwise_mismatches(out, ref) == {}
+    variants = [ca.VARIANT_KSEG]
+    if case.startswith("ncldtop"):
+        variants += [ca.VARIANT_KCACHE, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE]
+    for variant in variants:
+        out = run_gpu(s, 300, 64, variant=variant)
+        assert bitwise_mismatches(out, ref) == {}, variant
 
 
 def test_dwarf_tolerance_vs_reference_h5(lib, ds):
