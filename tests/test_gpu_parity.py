@@ -384,30 +384,31 @@ def test_host_pipeline_fp32(lib, ds):
 
 # ---- shapes beyond the reference's: other KLEV, tiny and ragged problems ----
 def sliced_levels(ds, lo_lev):
-    """The bottom KLEV-lo_lev levels of the state as a standalone column
-    (half-level pressures sliced to match)."""
-    s = ds.copy()
-    for name, kind in {**ca.INPUT_FIELDS, **ca.AEROSOL_FIELDS, **ca.INOUT_FIELDS}.items():
-        if name not in s.inputs:
-            continue
-        a = s.inputs[name]
-        if kind == "2d":
-            s.inputs[name] = np.ascontiguousarray(a[lo_lev:])
-        elif kind == "2dh":
-            s.inputs[name] = np.ascontiguousarray(a[lo_lev:])
-        elif kind == "3d":
-            s.inputs[name] = np.ascontiguousarray(a[:, lo_lev:])
-    s.klev = ds.klev - lo_lev
-    s.reference = {}
-    return s
+    import make_fixtures as mf
+    return mf.sliced_levels(ds, lo_lev)
 
 
+@pytest.mark.parametrize("klev", [60, 3, 16, 274])
 @pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE])
-def test_other_klev_vs_oracle(lib, ds, oracle_mod, variant):
-    s = sliced_levels(ds, 77)                          # KLEV = 60
+def test_other_klev_vs_oracle(lib, ds, oracle_mod, variant, klev):
+    """Shallow columns (the bottom 60, 16 or 3 levels; NCLDTOP 2 for the last
+    two) and a deep one (274 levels: every layer split in two), bit for bit.
+    SCC_PRIVATE's private arrays are sized for KLEV <= 137 (as the reference
+    CUDA SCC kernel's): deeper columns are rejected."""
+    import make_fixtures as mf
+    if klev == 274:
+        s = mf.refined_levels(ds, 2)
+    else:
+        s = sliced_levels(ds, ds.klev - klev)
+        if klev < 60:
+            s.params["ncldtop"] = 2
+    if variant == ca.VARIANT_SCC_PRIVATE and klev > 137:
+        with pytest.raises(ca.CloudscError):
+            run_gpu(s, 300, 64, variant=variant)
+        return
     out = run_gpu(s, 300, 64, variant=variant)
     ref = oracle_outputs(oracle_mod, s, 300, 64)
-    assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "klev 60")
+    assert bitwise_mismatches(out, ref) == {}
 
 
 @pytest.mark.parametrize("ngptot,nproma", [(1, 1), (1, 64), (5, 256), (127, 64), (257, 256), (64, 32)])
@@ -417,7 +418,7 @@ def test_tiny_and_ragged(lib, ds, oracle_mod, ngptot, nproma, variant):
     ref = oracle_outputs(oracle_mod, ds, ngptot, nproma)
     for _, k in ca.VALIDATED:
         assert out[k].shape == ref[k].shape
-    assert_close(field_report(out, ref), RELL1_FP64, MAXREL_FP64, "%d/%d" % (ngptot, nproma))
+    assert bitwise_mismatches(out, ref) == {}, (ngptot, nproma)
 
 
 def test_invalid_arguments(lib, ds):

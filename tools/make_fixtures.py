@@ -135,6 +135,49 @@ def with_aerosols(ds, seed=11):
     s.reference = {}
     return s
 
+def sliced_levels(ds, lo_lev):
+    """The bottom KLEV-lo_lev levels of the state as a standalone column
+    (half-level pressures sliced to match)."""
+    import cloudsc_amd as ca
+    s = ds.copy()
+    for name, kind in {**ca.INPUT_FIELDS, **ca.AEROSOL_FIELDS, **ca.INOUT_FIELDS}.items():
+        if name not in s.inputs:
+            continue
+        a = s.inputs[name]
+        if kind in ("2d", "2dh"):
+            s.inputs[name] = np.ascontiguousarray(a[lo_lev:])
+        elif kind == "3d":
+            s.inputs[name] = np.ascontiguousarray(a[:, lo_lev:])
+    s.klev = ds.klev - lo_lev
+    s.reference = {}
+    return s
+
+
+def refined_levels(ds, factor=2):
+    """A deeper column (KLEV * factor levels): every layer split into `factor`
+    equal-pressure sublayers -- full-level fields repeated, half-level pressures
+    interpolated linearly between the original interfaces."""
+    import cloudsc_amd as ca
+    s = ds.copy()
+    kinds = {**ca.INPUT_FIELDS, **ca.AEROSOL_FIELDS, **ca.INOUT_FIELDS}
+    for name, kind in kinds.items():
+        if name not in s.inputs:
+            continue
+        a = s.inputs[name]
+        if kind == "2d":
+            s.inputs[name] = np.ascontiguousarray(np.repeat(a, factor, axis=0))
+        elif kind == "3d":
+            s.inputs[name] = np.ascontiguousarray(np.repeat(a, factor, axis=1))
+        elif kind == "2dh":
+            lo, hi = a[:-1], a[1:]
+            sub = [lo + (hi - lo) * (j / factor) for j in range(factor)]
+            inter = np.stack(sub, axis=1).reshape((a.shape[0] - 1) * factor, *a.shape[1:])
+            s.inputs[name] = np.ascontiguousarray(np.concatenate([inter, a[-1:]], axis=0))
+    s.klev = ds.klev * factor
+    s.reference = {}
+    return s
+
+
 def make_scenarios():
     import oracle  # the compiled reference kernel (oracle/_ref)
     if not oracle.ref_available():
