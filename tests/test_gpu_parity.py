@@ -605,3 +605,31 @@ def test_bitwise_full_size_vs_oracle(lib, ds, oracle_mod):
     out = run_gpu(ds, 163840, 64, variant=ca.VARIANT_KSEG)
     ref = oracle_outputs(oracle_mod, ds, 163840, 64)
     assert bitwise_mismatches(out, ref) == {}
+
+
+@pytest.mark.parametrize("case", ["ncldtop2", "ncldtop138", "klev3", "klev274", "aerosol", "nssopt3"])
+@pytest.mark.parametrize("variant", [ca.VARIANT_KSEG, ca.VARIANT_KCACHE, ca.VARIANT_SCC])
+def test_bitwise_fp32_other_configurations(lib, ds, oracle_mod, case, variant):
+    """fp32 against the fp32 restatement on the configurations the fp64 suite
+    pins against the reference kernel (parity-unpinned beyond the restatement:
+    the reference has no fp32 C kernel)."""
+    import make_fixtures as mf
+    if case.startswith("ncldtop"):
+        s = ds.copy()
+        s.params["ncldtop"] = int(case[len("ncldtop"):])
+    elif case == "klev3":
+        s = sliced_levels(ds, ds.klev - 3)
+        s.params["ncldtop"] = 2
+    elif case == "klev274":
+        s = mf.refined_levels(ds, 2)
+    elif case == "aerosol":
+        s = mf.with_aerosols(ds)
+    else:
+        s = ds.copy()
+        s.params["nssopt"] = 3
+    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=variant)
+    ref = oracle_outputs(oracle_mod, s, 300, 64, precision=ca.FP32)
+    for _, k in ca.VALIDATED:
+        a = np.ascontiguousarray(out[k], dtype=np.float32).view(np.uint32)
+        r = np.ascontiguousarray(ref[k], dtype=np.float32).view(np.uint32)
+        assert np.array_equal(a, r), (k, int(np.count_nonzero(a != r)))
