@@ -527,7 +527,8 @@ def test_bitwise_random_perturbations(lib, ds, oracle_mod, seed):
 
 
 @pytest.mark.parametrize("case", ["nssopt0", "nssopt2", "nssopt3", "aerosol", "klev60", "divisor_params",
-                                  "ncldtop2", "ncldtop40", "ncldtop120", "ncldtop137", "ncldtop138"])
+                                  "ncldtop2", "ncldtop40", "ncldtop120", "ncldtop137", "ncldtop138",
+                                  "cold", "dry", "moist"])
 def test_bitwise_other_configurations(lib, ds, oracle_mod, case):
     import make_fixtures as mf
     if case.startswith("ncldtop"):
@@ -545,11 +546,13 @@ def test_bitwise_other_configurations(lib, ds, oracle_mod, case):
             s.params[name] = s.params[name] * f
     elif case == "aerosol":
         s = mf.with_aerosols(ds)
+    elif case in ("cold", "dry", "moist"):
+        s = mf.shifted(ds, case)
     else:
         s = sliced_levels(ds, 77)
     ref = oracle_outputs(oracle_mod, s, 300, 64)
     variants = [ca.VARIANT_KSEG]
-    if case.startswith("ncldtop"):
+    if case.startswith("ncldtop") or case in ("cold", "dry", "moist"):
         variants += [ca.VARIANT_KCACHE, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE]
     for variant in variants:
         out = run_gpu(s, 300, 64, variant=variant)

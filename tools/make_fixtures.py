@@ -118,6 +118,28 @@ def perturbed(ds, seed):
     return s
 
 
+def shifted(ds, kind):
+    """Regime copies of the state: "cold" (every temperature 25 K lower: ice
+    only, homogeneous freezing below RTHOMO, Koop-limited supersaturation),
+    "dry" (humidity x0.1, no condensate: the tidy-up and evaporation paths),
+    "moist" (humidity x1.6 and ten times the condensate: supersaturation
+    adjustment, autoconversion, precipitation everywhere)."""
+    s = ds.copy()
+    if kind == "cold":
+        s.inputs["pt"] = s.inputs["pt"] - 25.0
+    elif kind == "dry":
+        s.inputs["pq"] = s.inputs["pq"] * 0.1
+        s.inputs["pclv"] = np.zeros_like(s.inputs["pclv"])
+        s.inputs["pa"] = np.zeros_like(s.inputs["pa"])
+    elif kind == "moist":
+        s.inputs["pq"] = s.inputs["pq"] * 1.6
+        s.inputs["pclv"] = s.inputs["pclv"] * 10.0
+    else:
+        raise ValueError(kind)
+    s.reference = {}
+    return s
+
+
 def with_aerosols(ds, seed=11):
     """Copy of the state with LAERICESED / LAERICEAUTO on and physically sized
     aerosol inputs (the shipped PRE_ICE / PICRIT_AER / PNICE are all zero, which
