@@ -735,45 +735,75 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // zsolqa[n][m] and its transpose zsolqa[m][n] (the diagonal twice).
     // The structurally-zero entries are kept as literal zeros so the
     // summation order (and hence rounding) matches the dense reference.
+    // Where the sinks do not exceed what is there, max(-psum, zmm) is zmm and
+    // the reference's ratio zmm/zmm is exactly 1 (zmm >= zepsec, finite): its
+    // scaling multiplies by 1 and changes no bit, so the division and the
+    // scaling run only where they can change something (a wave skips them
+    // when none of its columns needs them).
     {
       real z = R(0.0), psum, zrat;
       // m = ql: zsolqa[n][ql] = {ll, il, rl, sl, vl}
       psum = R(0.0) + sa_ll; psum = psum + (-sa_li); psum = psum + (-sa_lr); psum = psum + (-sa_ls); psum = psum + (-sa_lv);
-      { const real zmm = fmax(zqx[QL], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
-      if (sa_ll < R(0.0)) { sa_ll = sa_ll * zrat; sa_ll = sa_ll * zrat; }
-      if (-sa_li < R(0.0)) sa_li = sa_li * zrat;
-      if (-sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
-      if (-sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
-      if (-sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
+      {
+        const real zmm = fmax(zqx[QL], zepsec), den = fmax(R(0.0) - psum, zmm);
+        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+          zrat = cl_div(zmm, den);
+          if (sa_ll < R(0.0)) { sa_ll = sa_ll * zrat; sa_ll = sa_ll * zrat; }
+          if (-sa_li < R(0.0)) sa_li = sa_li * zrat;
+          if (-sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
+          if (-sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
+          if (-sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
+        }
+      }
       // m = qi: {li, ii, ri, si(0), vi}
       psum = R(0.0) + sa_li; psum = psum + sa_ii; psum = psum + (-sa_ir); psum = psum + z; psum = psum + (-sa_iv);
-      { const real zmm = fmax(zqx[QI], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
-      if (sa_li < R(0.0)) sa_li = sa_li * zrat;
-      if (sa_ii < R(0.0)) { sa_ii = sa_ii * zrat; sa_ii = sa_ii * zrat; }
-      if (-sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
-      if (-sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
+      {
+        const real zmm = fmax(zqx[QI], zepsec), den = fmax(R(0.0) - psum, zmm);
+        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+          zrat = cl_div(zmm, den);
+          if (sa_li < R(0.0)) sa_li = sa_li * zrat;
+          if (sa_ii < R(0.0)) { sa_ii = sa_ii * zrat; sa_ii = sa_ii * zrat; }
+          if (-sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
+          if (-sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
+        }
+      }
       // m = qr: {lr, ir, rr, sr, vr}
       psum = R(0.0) + sa_lr; psum = psum + sa_ir; psum = psum + sa_rr; psum = psum + sa_sr; psum = psum + (-sa_rv);
-      { const real zmm = fmax(zqx[QR], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
-      if (sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
-      if (sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
-      if (sa_rr < R(0.0)) { sa_rr = sa_rr * zrat; sa_rr = sa_rr * zrat; }
-      if (sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
-      if (-sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
+      {
+        const real zmm = fmax(zqx[QR], zepsec), den = fmax(R(0.0) - psum, zmm);
+        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+          zrat = cl_div(zmm, den);
+          if (sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
+          if (sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
+          if (sa_rr < R(0.0)) { sa_rr = sa_rr * zrat; sa_rr = sa_rr * zrat; }
+          if (sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
+          if (-sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
+        }
+      }
       // m = qs: {ls, is(0), rs, ss, vs}
       psum = R(0.0) + sa_ls; psum = psum + z; psum = psum + (-sa_sr); psum = psum + sa_ss; psum = psum + (-sa_sv);
-      { const real zmm = fmax(zqx[QS], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
-      if (sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
-      if (-sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
-      if (sa_ss < R(0.0)) { sa_ss = sa_ss * zrat; sa_ss = sa_ss * zrat; }
-      if (-sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
+      {
+        const real zmm = fmax(zqx[QS], zepsec), den = fmax(R(0.0) - psum, zmm);
+        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+          zrat = cl_div(zmm, den);
+          if (sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
+          if (-sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
+          if (sa_ss < R(0.0)) { sa_ss = sa_ss * zrat; sa_ss = sa_ss * zrat; }
+          if (-sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
+        }
+      }
       // m = qv: {lv, iv, rv, sv, vv(0)}
       psum = R(0.0) + sa_lv; psum = psum + sa_iv; psum = psum + sa_rv; psum = psum + sa_sv; psum = psum + z;
-      { const real zmm = fmax(zqx[QV], zepsec); zrat = cl_div(zmm, fmax(R(0.0) - psum, zmm)); }
-      if (sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
-      if (sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
-      if (sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
-      if (sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
+      {
+        const real zmm = fmax(zqx[QV], zepsec), den = fmax(R(0.0) - psum, zmm);
+        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+          zrat = cl_div(zmm, den);
+          if (sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
+          if (sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
+          if (sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
+          if (sa_sv < R(0.0)) sa_sv = sa_sv * zrat;
+        }
+      }
     }
 
     // 5.2.2 implicit solver (:2294-2397).  With the zsolqb sparsity above,
