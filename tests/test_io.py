@@ -320,3 +320,54 @@ def test_python_loader_reads_serialbox(ds):
     sb = ca.read_serialbox_params(DATA)
     assert txt == sb
     assert ds.params == sb
+
+
+def _corruptions(seed=20261016):
+    """(file, description, mutator(bytes) -> bytes) for the metadata and data files."""
+    import random
+    rng = random.Random(seed)
+    cases = []
+    for name in ("MetaData-input.json", "ArchiveMetaData-input.json", "MetaData-reference.json",
+                 "ArchiveMetaData-reference.json", "manifest.json"):
+        size = os.path.getsize(os.path.join(DATA, name))
+        for frac in (0.0, 0.1, 0.5, 0.9, 0.999):
+            n = int(size * frac)
+            cases.append((name, "truncated at %d" % n, lambda b, n=n: b[:n]))
+        for _ in range(4):
+            pos = rng.randrange(size)
+            junk = bytes(rng.choice(b'{}[]":,0123456789-eE.xyz \x00\xff') for _ in range(rng.randint(1, 8)))
+            cases.append((name, "junk at %d" % pos, lambda b, pos=pos, junk=junk: b[:pos] + junk + b[pos + len(junk):]))
+        cases.append((name, "digits doubled", lambda b: b.replace(b"1", b"11")))
+        cases.append((name, "numbers as strings", lambda b: b.replace(b": 1", b': "1"')))
+        cases.append((name, "empty", lambda b: b""))
+    for name in ("input_PT.dat", "input_KTYPE.dat", "input_PCLV.dat", "reference_PLUDE.dat"):
+        cases.append((name, "empty", lambda b: b""))
+        cases.append((name, "one byte more", lambda b: b + b"\x00"))
+        cases.append((name, "one value less", lambda b: b[:-8]))
+    return cases
+
+
+def test_readers_survive_corrupted_metadata(io, tmp_path):
+    """I/O hardening: every reader returns 0 or CLOUDSC_EIO (-6)
+    with a message -- never a crash -- on truncated, garbled, empty and
+    mis-sized metadata and data files (each case in a child process, so a
+    crash is seen as a signal)."""
+    import sys
+    child = os.path.join(REPO, "tests", "io_fuzz_child.py")
+    base = tmp_path / "sb"
+    shutil.copytree(DATA, base)
+    for p in base.iterdir():
+        os.chmod(p, 0o644)
+    bad = []
+    for name, what, mutate in _corruptions():
+        f = base / name
+        orig = f.read_bytes()
+        try:
+            f.write_bytes(mutate(orig))
+            r = subprocess.run([sys.executable, child, str(base)], capture_output=True, text=True, timeout=120)
+            rcs = r.stdout.split()
+            if r.returncode != 0 or len(rcs) != 3 or any(x not in ("0", "-6") for x in rcs):
+                bad.append((name, what, r.returncode, r.stdout.strip(), r.stderr.strip()[-300:]))
+        finally:
+            f.write_bytes(orig)
+    assert bad == [], bad[:5]
