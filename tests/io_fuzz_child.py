@@ -36,5 +36,19 @@ def main(path):
     print(" ".join(str(r) for r in rcs))
 
 
+def main_hdf5(inp, ref):
+    lib = C.CDLL(IO_LIB)
+    lib.cloudsc_io_load_hdf5.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Dataset)]
+    lib.cloudsc_io_free.argtypes = [C.POINTER(Dataset)]
+    d = Dataset()
+    rc = lib.cloudsc_io_load_hdf5(inp.encode(), ref.encode() if ref else None, C.byref(d))
+    if rc == 0:
+        lib.cloudsc_io_free(C.byref(d))
+    print(rc)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if sys.argv[1] == "--hdf5":
+        main_hdf5(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    else:
+        main(sys.argv[1])

@@ -371,3 +371,34 @@ def test_readers_survive_corrupted_metadata(io, tmp_path):
         finally:
             f.write_bytes(orig)
     assert bad == [], bad[:5]
+
+
+def test_hdf5_reader_survives_corrupted_files(io, tmp_path):
+    """The read-only HDF5 reader on truncated and bit-flipped input.h5 /
+    reference.h5: 0 or CLOUDSC_EIO, never a crash (child process per case)."""
+    import random
+    import sys
+    need_hdf5(io)
+    child = os.path.join(REPO, "tests", "io_fuzz_child.py")
+    d = load_raw(io)
+    try:
+        inp, ref = tmp_path / "input.h5", tmp_path / "reference.h5"
+        assert io.cloudsc_io_write_hdf5(C.byref(d), str(inp).encode(), str(ref).encode()) == 0
+    finally:
+        io.cloudsc_io_free(C.byref(d))
+    rng = random.Random(7)
+    bad = []
+    for target in (inp, ref):
+        orig = target.read_bytes()
+        cases = [("truncated at %d" % n, orig[:n]) for n in (0, 100, 2048, len(orig) // 2, len(orig) - 1)]
+        for _ in range(8):
+            pos = rng.randrange(len(orig))
+            cases.append(("byte %d flipped" % pos, orig[:pos] + bytes([orig[pos] ^ 0xFF]) + orig[pos + 1:]))
+        for what, data in cases:
+            target.write_bytes(data)
+            r = subprocess.run([sys.executable, child, "--hdf5", str(inp), str(ref)], capture_output=True, text=True,
+                               timeout=120)
+            if r.returncode != 0 or r.stdout.strip() not in ("0", "-6"):
+                bad.append((target.name, what, r.returncode, r.stdout.strip(), r.stderr.strip()[-300:]))
+        target.write_bytes(orig)
+    assert bad == [], bad[:5]
