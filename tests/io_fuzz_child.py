@@ -10,7 +10,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "dwarf-p-cloudsc_amd"))
 import cloudsc_amd as ca  # noqa: E402  (the Params mirror only; no GPU library is loaded)
 
-IO_LIB = os.path.join(REPO, "dwarf-p-cloudsc_amd", "libcloudsc_io.so")
+IO_LIB = os.environ.get("CLOUDSC_IO_LIB", os.path.join(REPO, "dwarf-p-cloudsc_amd", "libcloudsc_io.so"))   # e.g. a sanitizer build
 NIN = 28
 
 
