@@ -230,6 +230,8 @@ def main():
                      "algorithmic_bytes_per_column": bpc,
                      "algorithmic_bytes_per_launch": bpc * args.ngptot},
     }
+    if traffic:   # the measured HBM bytes of one launch over this run's kernel time
+        line["roofline"]["traffic_gbs"] = round(traffic / (k_avg_ms * 1e6), 1)
     if peak_meas:
         line["roofline"]["achievable_peak"] = {
             "value": round(peak_meas, 1), "unit": "GB/s",
