@@ -406,6 +406,8 @@ def gpu_lib(path: Optional[str] = None):
                                     C.POINTER(C.c_double)]
     lib.cloudsc_debug_set_kseg_spin_limit.argtypes = [C.c_longlong]
     lib.cloudsc_debug_set_kseg_schedule.argtypes = [C.c_int, C.c_int]
+    lib.cloudsc_debug_host_pipeline_mapping.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    lib.cloudsc_debug_host_pinned.argtypes = [C.c_void_p, C.c_longlong]
     _lib = lib
     return lib
 
@@ -628,6 +630,22 @@ class HostPipeline:
 
     def outputs(self) -> Dict[str, np.ndarray]:
         return state_outputs_to_template(self.state.arrays, self.ngptot)
+
+    def mapping(self):
+        """(arrays, arrays NOT covered by one pinned mapping) -- the pinning
+        invariant of cloudsc_host_pipeline_create (cloudsc_debug_host_pipeline_mapping)."""
+        n, bad = C.c_int(), C.c_int()
+        check(self.lib.cloudsc_debug_host_pipeline_mapping(self.h, C.byref(n), C.byref(bad)))
+        return n.value, bad.value
+
+    def host_arrays(self):
+        """(pointer, bytes) of every host array handed to the pipeline."""
+        out = []
+        for name, _ in Fields._fields_:
+            p = getattr(self._fields, name)
+            if p:
+                out.append((p, self.state.arrays[name].nbytes))
+        return out
 
     def close(self) -> None:
         if getattr(self, "h", None):

@@ -124,34 +124,52 @@ KArgs<double> host_args(const cloudsc_fields_t* f, int ngptot, int nproma, int k
 
 }  // namespace
 
-extern "C" int cloudsc_cpu_run(int nthreads, int ngptot, int nproma, int klev, const cloudsc_params_t* params,
-                               const cloudsc_fields_t* f, double* seconds) {
+extern "C" int cloudsc_cpu_run_threads(int nthreads, int ngptot, int nproma, int klev,
+                                       const cloudsc_params_t* params, const cloudsc_fields_t* f, double* seconds,
+                                       double* thread_seconds, int* thread_blocks, int* thread_columns) {
   int rc = cloudsc_impl::check_params(params);
   if (rc) return rc;
   if (!f || !cloudsc_impl::fields_complete(f) || ngptot <= 0 || nproma <= 0 || klev < 2) return CLOUDSC_EINVAL;
   const bool aer = params->laericesed || params->laericeauto;
   if (aer && (!f->pre_ice || !f->picrit_aer || !f->pnice)) return CLOUDSC_EINVAL;
+  if (nthreads <= 0 && (thread_seconds || thread_blocks || thread_columns)) return CLOUDSC_EINVAL;
   const DevParams<double> c = fold_params<double>(*params);
   const KArgs<double> A = host_args(f, ngptot, nproma, klev);
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
   if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+  const int nreq = nthreads;                 // the caller's per-thread arrays have nreq entries
   nthreads = std::min(nthreads, nblocks);
+  for (int t = 0; t < nreq; t++) {           // threads beyond the block count do nothing
+    if (thread_seconds) thread_seconds[t] = 0.0;
+    if (thread_blocks) thread_blocks[t] = 0;
+    if (thread_columns) thread_columns[t] = 0;
+  }
   std::atomic<int> next{0};
-  auto worker = [&]() {
+  // per thread, as the C dwarf's zinfo (cloudsc_driver.c:185-228): its own
+  // wall time, NPROMA blocks taken (icalls) and columns computed (igpc)
+  auto worker = [&](int tid) {
+    const auto s0 = std::chrono::steady_clock::now();
     std::vector<HostColumn<double>> col((size_t)nproma);
+    int icalls = 0, igpc = 0;
     for (int b = next.fetch_add(1); b < nblocks; b = next.fetch_add(1)) {
       if (aer) run_block<double, true>(c, A, b, col);
       else run_block<double, false>(c, A, b, col);
+      icalls++;
+      igpc += std::min(nproma, ngptot - b * nproma);
     }
+    const auto s1 = std::chrono::steady_clock::now();
+    if (thread_seconds) thread_seconds[tid] = std::chrono::duration<double>(s1 - s0).count();
+    if (thread_blocks) thread_blocks[tid] = icalls;
+    if (thread_columns) thread_columns[tid] = igpc;
   };
   const auto t0 = std::chrono::steady_clock::now();
   if (nthreads == 1) {
-    worker();
+    worker(0);
   } else {
     std::vector<std::thread> pool;
     pool.reserve((size_t)nthreads);
     try {
-      for (int t = 0; t < nthreads; t++) pool.emplace_back(worker);
+      for (int t = 0; t < nthreads; t++) pool.emplace_back(worker, t);
     } catch (...) {
       rc = CLOUDSC_ENOMEM;          // the threads already started finish the blocks
     }
@@ -160,4 +178,9 @@ extern "C" int cloudsc_cpu_run(int nthreads, int ngptot, int nproma, int klev, c
   const auto t1 = std::chrono::steady_clock::now();
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
   return rc;
+}
+
+extern "C" int cloudsc_cpu_run(int nthreads, int ngptot, int nproma, int klev, const cloudsc_params_t* params,
+                               const cloudsc_fields_t* f, double* seconds) {
+  return cloudsc_cpu_run_threads(nthreads, ngptot, nproma, klev, params, f, seconds, nullptr, nullptr, nullptr);
 }

@@ -301,14 +301,24 @@ static int jvalue(jparser *j, jv *v, int depth) {
     }
   }
   if (c == '"') { v->type = 3; v->str = jstring(j); return v->str ? 0 : (j->err = 1); }
-  if (!strncmp(j->p, "true", 4)) { v->type = 1; v->num = 1; j->p += 4; return 0; }
-  if (!strncmp(j->p, "false", 5)) { v->type = 1; v->num = 0; j->p += 5; return 0; }
-  if (!strncmp(j->p, "null", 4)) { v->type = 0; j->p += 4; return 0; }
+  /* the text is not NUL-terminated: every look-ahead is bounded by j->end */
+  const size_t left = (size_t)(j->end - j->p);
+  if (left >= 4 && !memcmp(j->p, "true", 4)) { v->type = 1; v->num = 1; j->p += 4; return 0; }
+  if (left >= 5 && !memcmp(j->p, "false", 5)) { v->type = 1; v->num = 0; j->p += 5; return 0; }
+  if (left >= 4 && !memcmp(j->p, "null", 4)) { v->type = 0; j->p += 4; return 0; }
+  /* a number: its characters copied into a NUL-terminated buffer first, so
+   * strtod cannot read past the end of a file truncated inside the number */
+  char num[64];
+  size_t n = 0;
+  while (n < left && n < sizeof(num) - 1 && strchr("+-0123456789.eE", j->p[n]) && j->p[n]) n++;
+  if (n == 0 || n == sizeof(num) - 1) return j->err = 1;
+  memcpy(num, j->p, n);
+  num[n] = 0;
   char *e = NULL;
-  v->num = strtod(j->p, &e);     /* decimal -> double, correctly rounded by the C library */
-  if (e == j->p) return j->err = 1;
+  v->num = strtod(num, &e);      /* decimal -> double, correctly rounded by the C library */
+  if (e == num) return j->err = 1;
   v->type = 2;
-  j->p = e;
+  j->p += e - num;
   return 0;
 }
 static const jv *jget(const jv *o, const char *key) {

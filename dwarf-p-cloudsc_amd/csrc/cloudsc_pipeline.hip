@@ -284,5 +284,25 @@ int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p) {
   return CLOUDSC_OK;
 }
 
+int cloudsc_debug_host_pipeline_mapping(const cloudsc_host_pipeline_t* p, int* n_arrays, int* n_not_one_mapping) {
+  if (!p || !n_arrays || !n_not_one_mapping) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(p->device));
+  const void* const* hf = (const void* const*)&p->host;
+  int n = 0, bad = 0;
+  for (int i = 0; i < kNumFields; i++) {
+    if (!hf[i]) continue;
+    n++;
+    if (!pinned_as_one(hf[i], field_bytes(p, i, p->nblocks))) bad++;
+  }
+  *n_arrays = n;
+  *n_not_one_mapping = bad;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_debug_host_pinned(const void* ptr, long long bytes) {
+  if (!ptr || bytes <= 0) return 0;
+  return pinned_as_one(ptr, (size_t)bytes) ? 1 : 0;
+}
+
 }  // extern "C"
 

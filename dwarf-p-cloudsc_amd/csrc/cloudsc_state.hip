@@ -16,17 +16,23 @@ using namespace cloudsc_impl;
 // ---------------------------------------------------------------------------
 // plumbing kernels: expansion and validation statistics
 // ---------------------------------------------------------------------------
-// dst[b][L][i] = src[L][(col_offset + b*nproma + i) % klon], L < nlev
+// dst[b][L][i] = src[L][(col_offset + b*nproma + i) % klon], L < nlev.
+// A 1-D grid strides over all nblocks*nlev*nproma elements with 64-bit
+// indices: no grid dimension carries the block count (HIP's y/z limit is
+// 65536 -- the CUDA driver's gridDim.z quirk, SURVEY.md Appendix B item 7,
+// cloudsc_driver.cu:391-397), and nlev*nproma may exceed 2^31 (685 species
+// levels x NPROMA > 3.1 M).
 template <typename T, typename S>
 __global__ void expand_kernel(T* __restrict__ dst, const S* __restrict__ src, int nlev, int klon,
                               int nproma, long long col_offset, long long nblocks) {
-  const long long b = blockIdx.y;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nlev * nproma; e += gridDim.x * blockDim.x) {
-    const int L = e / nproma, i = e - L * nproma;
+  const long long per = (long long)nlev * nproma, total = per * nblocks;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const long long b = e / per, r = e - b * per;
+    const long long L = r / nproma, i = r - L * nproma;
     const long long g = col_offset + b * nproma + i;
-    dst[(size_t)b * nlev * nproma + e] = (T)src[(size_t)L * klon + (size_t)(g % klon)];
+    dst[e] = (T)src[L * klon + g % klon];
   }
-  (void)nblocks;
 }
 
 // One workgroup per NPROMA block: min/max of the field, max|d|, sum|d|, sum|ref|
@@ -38,12 +44,13 @@ __global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld
   const long long b = blockIdx.x;
   const long long bsize = (ngptot - b * nproma) < nproma ? (ngptot - b * nproma) : nproma;
   double mn = __DBL_MAX__, mx = -__DBL_MAX__, me = 0.0, es = 0.0, rs = 0.0;
-  for (int e = threadIdx.x; e < nlev * nproma; e += blockDim.x) {
-    const int L = e / nproma, i = e - L * nproma;
+  const long long per = (long long)nlev * nproma;   // 64-bit: may exceed 2^31 at large NPROMA
+  for (long long e = threadIdx.x; e < per; e += blockDim.x) {
+    const long long L = e / nproma, i = e - L * nproma;
     if (i >= bsize) continue;
     const long long g = col_offset + b * nproma + i;
-    const double v = (double)fld[(size_t)b * nlev * nproma + e];
-    const double r = ref[(size_t)L * klon + (size_t)(g % klon)];
+    const double v = (double)fld[b * per + e];
+    const double r = ref[L * klon + g % klon];
     const double d = fabs(v - r);
     mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, d); es += d; rs += fabs(r);
   }
@@ -117,8 +124,10 @@ int expand_into(cloudsc_gpu_state* s, void* dst, const void* host_src, int nlev,
   HIPCHK(hipMalloc(&d_src, src_bytes));
   hipError_t e = hipMemcpyAsync(d_src, host_src, src_bytes, hipMemcpyHostToDevice, s->stream);
   if (e == hipSuccess) {
-    const int per = nlev * s->nproma;
-    dim3 grid((per + 255) / 256, s->nblocks);
+    // 1-D grid, enough workgroups to fill the chip, the kernel strides the rest
+    const long long total = (long long)nlev * s->nproma * s->nblocks;
+    const long long want = (total + 255) / 256;
+    dim3 grid((unsigned)(want < 16384 ? want : 16384));
     if (is_int)
       hipLaunchKernelGGL((expand_kernel<int, int>), grid, dim3(256), 0, s->stream, (int*)dst, (const int*)d_src,
                          nlev, s->klon, s->nproma, s->col_offset, (long long)s->nblocks);
@@ -266,9 +275,10 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
   for (auto& x : ev) (void)hipEventDestroy(x);
   if (rc == CLOUDSC_OK && variant == CLOUDSC_VARIANT_KSEG) {
     // a segment whose predecessor never arrived gives up after a bounded spin
-    // and counts itself: its results are invalid.  The counter is re-zeroed by
-    // every launch, and a timed-out hand-off leaves the wrong carried state in
-    // every later step too, so the last step's count is the one to read.
+    // and counts itself in the workspace's error word: its results are
+    // invalid.  The count accumulates over the reps of this call (the word is
+    // sticky across launches); kseg_check reads and clears it, and any failure
+    // resets kseg_epoch (below), so the next call zeroes the workspace again.
     rc = kseg_check(s->device, s->stream, scratch);
   }
   if (rc != CLOUDSC_OK) s->kseg_epoch.ready = false;   // zero the workspace again before the next launch

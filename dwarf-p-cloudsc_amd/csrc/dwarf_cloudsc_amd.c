@@ -292,13 +292,25 @@ static int run_host(const options_t *o, const cloudsc_dataset_t *ds) {
   if (!rc && !cpu) rc = cloudsc_host_pipeline_create(&pipe, 0, o->precision, o->ngptot, o->nproma, ds->klev,
                                                      o->chunk_blocks, o->nstreams, &f);
   double total_ms = 0.0;
+  /* --variant cpu: the per-thread record of the C dwarf (zinfo), summed over the timed steps */
+  const int nth = o->numomp;
+  double *th_s = cpu ? (double *)calloc((size_t)nth, sizeof(double)) : NULL;
+  double *th_step = cpu ? (double *)calloc((size_t)nth, sizeof(double)) : NULL;
+  int *th_blk = cpu ? (int *)calloc((size_t)nth, sizeof(int)) : NULL;
+  int *th_col = cpu ? (int *)calloc((size_t)nth, sizeof(int)) : NULL;
+  int *th_blk_step = cpu ? (int *)calloc((size_t)nth, sizeof(int)) : NULL;
+  int *th_col_step = cpu ? (int *)calloc((size_t)nth, sizeof(int)) : NULL;
+  if (cpu && (!th_s || !th_step || !th_blk || !th_col || !th_blk_step || !th_col_step)) rc = CLOUDSC_ENOMEM;
   for (int r = 0; r < o->warmup + o->reps && !rc; r++) {
     memcpy(f.plude, plude0, plude_bytes);                 /* INOUT restored, outside the timing */
     double ms = 0.0;
     if (cpu) {
       double secs = 0.0;
-      rc = cloudsc_cpu_run(o->numomp, o->ngptot, o->nproma, ds->klev, &ds->params, &f, &secs);
+      rc = cloudsc_cpu_run_threads(nth, o->ngptot, o->nproma, ds->klev, &ds->params, &f, &secs, th_step,
+                                   th_blk_step, th_col_step);
       ms = 1e3 * secs;
+      if (r >= o->warmup)
+        for (int t = 0; t < nth; t++) { th_s[t] += th_step[t]; th_blk[t] += th_blk_step[t]; th_col[t] += th_col_step[t]; }
     } else {
       rc = cloudsc_host_pipeline_run(pipe, o->variant, &ms);
     }
@@ -313,6 +325,14 @@ static int run_host(const options_t *o, const cloudsc_dataset_t *ds) {
     printf(" Reference MFLOP count for 100 columns : %12.8f\n", 1.0e-06 * ZHPM);
     printf(" %10s%10s%10s%10s%10s %4s : %10s%10s%10s\n", "NUMOMP", "NGPTOT", "#GP-cols", "#BLKS", "NPROMA",
            "tid#", "Time(msec)", "MFlops/s", "col/s");
+    /* per-thread rows (cloudsc_driver.c:238-253): columns and blocks of the last
+     * step; time, MFlops/s and col/s over all timed steps like the TOTAL row */
+    for (int t = 0; cpu && t < nth; t++) {
+      const double tl = th_s[t], zfrac = (double)th_col[t] / cols;
+      printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d @ core#\n", o->numomp, o->ngptot, th_col_step[t],
+             th_blk_step[t], o->nproma, t, (int)(tl * 1000.),
+             tl > 0 ? (int)(1.0e-06 * zfrac * ZHPM * (cols / 100.) / tl) : 0, tl > 0 ? (int)(cols / tl) : 0);
+    }
     printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d TOTAL\n", o->numomp, o->ngptot, o->ngptot, nb, o->nproma, -1,
            (int)(t * 1000.), (int)(1.0e-06 * ZHPM * (cols / 100.) / t), (int)(cols / t));
     if (cpu)
@@ -350,6 +370,7 @@ static int run_host(const options_t *o, const cloudsc_dataset_t *ds) {
   }
   for (int i = 0; i < 48; i++) free(fp[i]);
   free(plude0);
+  free(th_s); free(th_step); free(th_blk); free(th_col); free(th_blk_step); free(th_col_step);
   return rc ? EXIT_FAILURE : (bad ? EXIT_FAILURE : EXIT_SUCCESS);
 }
 
@@ -484,12 +505,16 @@ int main(int argc, char **argv) {
   printf(" Reference MFLOP count for 100 columns : %12.8f\n", 1.0e-06 * ZHPM);
   printf(" %10s%10s%10s%10s%10s %4s : %10s%10s%10s\n", "NUMOMP", "NGPTOT", "#GP-cols", "#BLKS", "NPROMA", "tid#",
          "Time(msec)", "MFlops/s", "col/s");
+  /* one row per shard, as the reference GPU driver prints one per host thread
+   * (cloudsc_driver.cu:462-477): tid# = the shard (its host thread), and the row
+   * ends in "@ core#" exactly as there, so JUBE's thr_time/thr_mflops patterns
+   * (benchmark/include/include_patternset.yml:161-162) match it */
   for (int d = 0; d < nused; d++) {
     const double tl = sh[d].t_end - sh[d].t_start;
     const int nbd = sh[d].ngptot / o.nproma + (sh[d].ngptot % o.nproma ? 1 : 0);
     const double c = (double)sh[d].ngptot * o.reps;
-    printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d @ gpu#\n", o.numomp, o.ngptot, sh[d].ngptot, nbd, o.nproma,
-           sh[d].device, (int)(tl * 1000.), tl > 0 ? (int)(1.0e-06 * ZHPM * (c / 100.) / tl) : 0,
+    printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d @ core#\n", o.numomp, o.ngptot, sh[d].ngptot, nbd, o.nproma,
+           d, (int)(tl * 1000.), tl > 0 ? (int)(1.0e-06 * ZHPM * (c / 100.) / tl) : 0,
            tl > 0 ? (int)(c / tl) : 0);
   }
   printf(" %10d%10d%10d%10d%10d %4d : %10d%10d%10d TOTAL\n", o.numomp, o.ngptot, o.ngptot, nblocks, o.nproma, -1,

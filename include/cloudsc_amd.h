@@ -7,7 +7,10 @@
  * a default set (cloudsc_gpu_init, used by cloudsc_gpu_run), and every state
  * and host pipeline owns a private copy, so states with different parameters
  * can be interleaved on one device.  One host thread per device -- or one
- * thread driving N devices -- is safe.
+ * thread driving N devices -- is safe.  cloudsc_gpu_init rewrites the device's
+ * default set in place: it must not race with cloudsc_gpu_run or
+ * cloudsc_host_pipeline_create on the same device from another thread (states
+ * and pipelines already created are unaffected).
  *
  * Which reference interface each declaration replaces (paths relative to the
  * lukasm91/dwarf-p-cloudsc checkout):
@@ -27,7 +30,7 @@
  *                         (src/cloudsc_c/cloudsc/cloudsc_driver.c:183-217, kernel
  *                         cloudsc_c.c:19-2587, declared cloudsc_c.h:18-29)
  *   cloudsc_gpu_run    <- cloudsc_c<<<grid,nproma>>>(...) (cloudsc_driver.cu:391-416)
- *   cloudsc_gpu_state_* <- the driver plumbing around the kernel: load+expand
+ *   cloudsc_state_*    <- the driver plumbing around the kernel: load+expand
  *                         (load_state.c:69-184,279), timing (cloudsc_driver.c:181-262),
  *                         validation (src/common/module/validate_mod.F90:118-296)
  *
@@ -157,8 +160,11 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t *params);
  * and per-block flags that are re-zeroed on `stream` before every launch, so one
  * workspace must not be shared by launches in flight on different streams.
  * nproma: 1..256 for KCACHE and SCC (one workgroup of nproma threads per
- * block), any positive value for KSEG (64-column sub-blocks); otherwise
- * CLOUDSC_EINVAL. */
+ * block), 1..2^24 for KSEG (64-column sub-blocks; all index arithmetic is
+ * 64-bit); otherwise CLOUDSC_EINVAL.
+ * A caller-owned KSEG workspace carries a sticky error word (below): zero it,
+ * or pass it through cloudsc_gpu_check, before reusing the memory for a new
+ * series of launches, or a stale count may surface as CLOUDSC_EHANDOFF. */
 int cloudsc_gpu_run(int device, void *stream, int precision, int variant,
                     int ngptot, int nproma, int klev,
                     const cloudsc_fields_t *device_fields, void *scratch);
@@ -216,6 +222,16 @@ long long cloudsc_abi_sizeof(int which);
  * NULL) = wall time of the block loop.  Needs no GPU. */
 int cloudsc_cpu_run(int nthreads, int ngptot, int nproma, int klev, const cloudsc_params_t *params,
                     const cloudsc_fields_t *host_fields, double *seconds);
+
+/* cloudsc_cpu_run with the C dwarf's per-thread record (zinfo,
+ * cloudsc_driver.c:185-228, printed as the "@ core#" rows at :238-253): for
+ * thread t < nthreads, thread_seconds[t] = its wall time, thread_blocks[t] =
+ * NPROMA blocks it took (icalls), thread_columns[t] = columns it computed
+ * (igpc).  Each array (may be NULL) holds nthreads entries; nthreads must be
+ * > 0 here.  Threads beyond the block count report zeros. */
+int cloudsc_cpu_run_threads(int nthreads, int ngptot, int nproma, int klev, const cloudsc_params_t *params,
+                            const cloudsc_fields_t *host_fields, double *seconds, double *thread_seconds,
+                            int *thread_blocks, int *thread_columns);
 
 /* ------------------------------------------------------------------------ */
 /* Dwarf plumbing on the device: expand a KLON-column template to NGPTOT      */
@@ -328,6 +344,20 @@ int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t **pipe, int device, int
 int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t *pipe, int variant, double *ms);
 
 int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t *pipe);
+
+/* Diagnostic: how the pipeline's host arrays are mapped for the device.
+ * *n_arrays = the number of non-NULL host arrays; *n_not_one_mapping = how many
+ * of them are NOT covered by a single pinned mapping from their first to their
+ * last byte (hipPointerGetAttributes at both ends, device addresses exactly
+ * bytes-1 apart).  0 is the invariant create establishes (merged page ranges,
+ * each registered once). */
+int cloudsc_debug_host_pipeline_mapping(const cloudsc_host_pipeline_t *pipe, int *n_arrays,
+                                        int *n_not_one_mapping);
+
+/* Diagnostic: 1 if [ptr, ptr+bytes) is currently pinned host memory reachable
+ * by the device as one mapping, 0 if not (e.g. after the pipeline that pinned
+ * it was destroyed). */
+int cloudsc_debug_host_pinned(const void *ptr, long long bytes);
 
 #ifdef __cplusplus
 }

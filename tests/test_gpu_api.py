@@ -8,8 +8,8 @@
   every path: the state API, the host pipeline, and cloudsc_gpu_check after a
   low-level cloudsc_gpu_run;
 * BASELINE.json configs 2 and 4 at their full size (163840 columns): SCC fp64
-  at NPROMA 128 bit-equal to KCACHE, and SCC-k-caching fp32 bit-equal to the
-  fp32 restatement (driver shape: src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:391-397).
+  (both temporaries forms) and KCACHE at NPROMA 128 bit-equal to the oracle, and
+  SCC-k-caching fp32 bit-equal to the fp32 restatement (driver shape: src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:391-397).
 """
 import ctypes as C
 
@@ -157,30 +157,28 @@ def test_handoff_timeout_host_pipeline(lib, ds, forced_handoff_failure):
         hp.close()
 
 
-def test_bitwise_scc_full_size(lib, ds):
-    """BASELINE.json config 2: SCC fp64 (HBM temporaries), NGPTOT 163840,
-    NPROMA 128 -- all 21 fields bit-equal to KCACHE on the same state (KCACHE is
-    pinned to the oracle at this size by test_bitwise_full_size_vs_oracle)."""
-    g = ca.GpuState(ds, 163840, 128)
-    try:
-        scc = outputs_of(g, ca.VARIANT_SCC)
-        kc = outputs_of(g, ca.VARIANT_KCACHE)
-    finally:
-        g.close()
-    assert bitwise_mismatches(scc, kc) == {}
+@pytest.fixture(scope="module")
+def oracle_163840_128(ds, oracle_mod):
+    """The oracle (the restatement pinned bit for bit to the reference kernel,
+    tests/test_oracle.py) at BASELINE.json config 2's full size: 163840
+    columns, NPROMA 128."""
+    return oracle_outputs(oracle_mod, ds, 163840, 128)
 
 
-def test_bitwise_scc_private_full_size(lib, ds):
-    """The reference's own SCC form (per-thread private arrays, cloudsc_c.cu:60-317)
-    at the full 163840 columns / NPROMA 128: 28.5 KB of private segment per
-    thread -- bit-equal to KCACHE on the same state."""
+@pytest.mark.parametrize("variant", [ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE, ca.VARIANT_KCACHE])
+def test_bitwise_config2_full_size_vs_oracle(lib, ds, oracle_163840_128, variant):
+    """BASELINE.json config 2 pinned directly: SCC fp64 with HBM temporaries
+    (the a4 hoist form), SCC with per-thread private arrays (the reference CUDA
+    SCC form, cloudsc_c.cu:60-317: 28.5 KB of private segment per thread) and
+    the k-caching kernel, each at NGPTOT 163840 / NPROMA 128 -- all 21 fields
+    bit-equal to the oracle at the same size and NPROMA (driver shape:
+    src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:391-397)."""
     g = ca.GpuState(ds, 163840, 128)
     try:
-        scp = outputs_of(g, ca.VARIANT_SCC_PRIVATE)
-        kc = outputs_of(g, ca.VARIANT_KCACHE)
+        out = outputs_of(g, variant)
     finally:
         g.close()
-    assert bitwise_mismatches(scp, kc) == {}
+    assert bitwise_mismatches(out, oracle_163840_128) == {}
 
 
 def test_bitwise_fp32_full_size(lib, ds, oracle_mod):
@@ -244,3 +242,25 @@ def test_kseg_consecutive_launches_on_one_workspace(lib, ds, nproma):
         assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=3), ref) == {}
     finally:
         g.close()
+
+
+def test_kseg_more_blocks_than_grid_y_limit(lib, ds):
+    """KSEG at 163840 columns with NPROMA 2: 81,920 blocks, more than HIP's
+    65,536 limit on a grid's y/z dimension.  The expansion and validation
+    kernels run 1-D grids with 64-bit indices (the CUDA driver's gridDim.z
+    quirk, SURVEY.md Appendix B item 7, cloudsc_driver.cu:391-397, avoided):
+    every field bit-equal to the NPROMA-64 run, and the on-device validation
+    statistics agree to the last bit with those of the NPROMA-64 state where
+    the block partition does not enter (min, max, max|d|)."""
+    out, stats = {}, {}
+    for nproma in (64, 2):
+        g = ca.GpuState(ds, 163840, nproma)
+        try:
+            out[nproma] = outputs_of(g, ca.VARIANT_KSEG)
+            stats[nproma] = g.validate()
+        finally:
+            g.close()
+    assert bitwise_mismatches(out[2], out[64]) == {}
+    for a, b in zip(stats[2], stats[64]):
+        assert a[:3] == b[:3]
+        assert abs(a[3] - b[3]) <= 1e-12 * max(abs(b[3]), 1e-300) and abs(a[4] - b[4]) <= 1e-12 * abs(b[4])

@@ -361,11 +361,19 @@ def test_host_pipeline_packed_arrays(lib, ds, variant):
     ref = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KCACHE)
     hp = ca.HostPipeline(ds, 1000, 128, chunk_blocks=5, nstreams=1, packed=True)
     try:
+        # the invariant whose violation faulted: every array resolves, from its
+        # first to its last byte, as ONE pinned mapping
+        n, bad = hp.mapping()
+        assert n >= 40 and bad == 0, (n, bad)
+        arrays = hp.host_arrays()
+        assert all(lib.cloudsc_debug_host_pinned(p, nb) == 1 for p, nb in arrays)
         hp.run(variant)
         hp.run(variant)
         out = hp.outputs()
     finally:
         hp.close()
+    # destroy leaves no registration behind (the buffer itself is still alive)
+    assert [p for p, nb in arrays if lib.cloudsc_debug_host_pinned(p, nb) != 0] == []
     for _, k in ca.VALIDATED:
         assert np.array_equal(out[k], ref[k]), k
 

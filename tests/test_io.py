@@ -340,6 +340,15 @@ def _corruptions(seed=20261016):
         cases.append((name, "digits doubled", lambda b: b.replace(b"1", b"11")))
         cases.append((name, "numbers as strings", lambda b: b.replace(b": 1", b': "1"')))
         cases.append((name, "empty", lambda b: b""))
+        # cut exactly inside a number and inside a literal: the parser's
+        # look-ahead (strtod, the true/false/null compares) must stop at the end
+        # of the buffer, which has no NUL terminator
+        digits = [i for i in range(1, size) if chr(open(os.path.join(DATA, name), "rb").read()[i - 1]).isdigit()]
+        for n in (digits[len(digits) // 2], digits[-1]) if digits else ():
+            cases.append((name, "truncated after a digit at %d" % n, lambda b, n=n: b[:n]))
+        cases.append((name, "ends in 'tr'", lambda b: b[:max(0, len(b) // 2)] + b' "x": tr'))
+        cases.append((name, "ends in 'fals'", lambda b: b[:max(0, len(b) // 3)] + b'[fals'))
+        cases.append((name, "ends in a long number", lambda b: b[:len(b) // 4] + b"1" * 200))
     for name in ("input_PT.dat", "input_KTYPE.dat", "input_PCLV.dat", "reference_PLUDE.dat"):
         cases.append((name, "empty", lambda b: b""))
         cases.append((name, "one byte more", lambda b: b + b"\x00"))
