@@ -140,7 +140,8 @@ class Reference(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("minval", C.c_double), ("maxval", C.c_double), ("maxerr", C.c_double),
-                ("errsum", C.c_double), ("refsum", C.c_double)]
+                ("errsum", C.c_double), ("refsum", C.c_double),
+                ("errsum_lo", C.c_double), ("refsum_lo", C.c_double)]
 
 
 # ---------------------------------------------------------------------------
@@ -560,7 +561,9 @@ class GpuState:
         ref = make_reference(ds, keep)
         st = (Stats * 21)()
         check(self.lib.cloudsc_state_validate(self.h, C.byref(ref), st))
-        return [(s.minval, s.maxval, s.maxerr, s.errsum, s.refsum) for s in st]
+        # (min, max, max|d|, sum|d|, sum|ref|, and the low parts of the two
+        # double-double sums: cloudsc_dist.combine_stats adds partials exactly)
+        return [(s.minval, s.maxval, s.maxerr, s.errsum, s.refsum, s.errsum_lo, s.refsum_lo) for s in st]
 
     def download(self, key: str) -> np.ndarray:
         idx = [k for _, k in VALIDATED].index(key)

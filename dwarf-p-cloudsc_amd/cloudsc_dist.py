@@ -97,11 +97,34 @@ class Control:
             self.dist = None
 
 
+def dd_add(a, b):
+    """Double-double sum of (hi, lo) pairs: the arithmetic of cloudsc_stats_combine
+    (cloudsc_state.hip) in IEEE doubles, so partial sums combine to the same
+    double in any grouping."""
+    s = a[0] + b[0]
+    bb = s - a[0]
+    e = (a[0] - (s - bb)) + (b[0] - bb)
+    t = e + (a[1] + b[1])
+    hi = s + t
+    return hi, t - (hi - s)
+
+
 def combine_stats(per_rank: Sequence[Sequence[Sequence[float]]]) -> List[Tuple[float, ...]]:
-    """min of mins, max of maxes, max of max|d|, sums of sum|d| and sum|ref|."""
+    """min of mins, max of maxes, max of max|d|, sums of sum|d| and sum|ref|.
+    Rows are (min, max, maxerr, errsum, refsum[, errsum_lo, refsum_lo]); with the
+    low parts the sums are combined as double-doubles (cloudsc_stats_t), so the
+    result does not depend on how the columns were split over ranks."""
     out = []
     for f in range(len(per_rank[0])):
         rows = [r[f] for r in per_rank]
-        out.append((min(r[0] for r in rows), max(r[1] for r in rows), max(r[2] for r in rows),
-                    sum(r[3] for r in rows), sum(r[4] for r in rows)))
+        if all(len(r) >= 7 for r in rows):
+            es, rs = (0.0, 0.0), (0.0, 0.0)
+            for r in rows:
+                es = dd_add(es, (r[3], r[5]))
+                rs = dd_add(rs, (r[4], r[6]))
+            out.append((min(r[0] for r in rows), max(r[1] for r in rows), max(r[2] for r in rows),
+                        es[0], rs[0], es[1], rs[1]))
+        else:
+            out.append((min(r[0] for r in rows), max(r[1] for r in rows), max(r[2] for r in rows),
+                        sum(r[3] for r in rows), sum(r[4] for r in rows)))
     return out

@@ -775,11 +775,23 @@ void cloudsc_io_expand(const void *src, int kind, int is_int, int klev, int klon
       }
 }
 
+/* (hi, lo) += x as a double-double (TwoSum + renormalisation), the same
+ * arithmetic as the device statistics (cloudsc_state.hip, dd_add) */
+static void dd_acc(double *hi, double *lo, double x) {
+  const double s = *hi + x, bb = s - *hi;
+  const double e = (*hi - (s - bb)) + (x - bb);
+  const double t = e + *lo;
+  const double h = s + t;
+  *lo = t - (h - s);
+  *hi = h;
+}
+
 void cloudsc_io_field_stats(const double *ref, int kind, int klev, int klon, const void *field, int elem_size,
                             int ngptot, int nproma, long long col_offset, cloudsc_stats_t *st) {
   const int nlev = kind_nlev(kind, klev);
   const long long nb = ngptot / nproma + (ngptot % nproma ? 1 : 0);
-  double mn = DBL_MAX, mx = -DBL_MAX, me = 0.0, es = 0.0, rs = 0.0;
+  double mn = DBL_MAX, mx = -DBL_MAX, me = 0.0;
+  double es = 0.0, es_lo = 0.0, rs = 0.0, rs_lo = 0.0;   /* double-double sums, as the device statistics */
   for (long long b = 0; b < nb; b++) {
     const long long bsize = ngptot - b * nproma < nproma ? ngptot - b * nproma : nproma;
     for (int l = 0; l < nlev; l++)
@@ -789,10 +801,13 @@ void cloudsc_io_field_stats(const double *ref, int kind, int klev, int klon, con
         const double v = elem_size == 8 ? ((const double *)field)[d] : (double)((const float *)field)[d];
         const double r = ref[(size_t)l * klon + (size_t)(g % klon)];
         const double df = fabs(v - r);
-        mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, df); es += df; rs += fabs(r);
+        mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, df);
+        dd_acc(&es, &es_lo, df);
+        dd_acc(&rs, &rs_lo, fabs(r));
       }
   }
   st->minval = mn; st->maxval = mx; st->maxerr = me; st->errsum = es; st->refsum = rs;
+  st->errsum_lo = es_lo; st->refsum_lo = rs_lo;
 }
 
 int cloudsc_io_load_dir(const char *dir, int with_reference, cloudsc_dataset_t *ds) {

@@ -35,15 +35,35 @@ __global__ void expand_kernel(T* __restrict__ dst, const S* __restrict__ src, in
   }
 }
 
+// Double-double accumulation of non-negative terms (Knuth's TwoSum, then a
+// renormalisation): hi + lo carries the sum to ~100 bits, so partial sums
+// combined in any grouping -- NPROMA blocks here, shards or ranks on the host --
+// round to the same double.  No FMA contraction applies (-ffp-contract=off),
+// and nothing here is reassociated (no fast-math).
+struct DD {
+  double hi, lo;
+};
+__host__ __device__ __forceinline__ DD dd_add(DD a, DD b) {
+  const double s = a.hi + b.hi;
+  const double bb = s - a.hi;
+  const double e = (a.hi - (s - bb)) + (b.hi - bb);   // TwoSum error of a.hi + b.hi
+  const double t = e + (a.lo + b.lo);
+  const double hi = s + t;
+  return {hi, t - (hi - s)};                          // FastTwoSum renormalisation
+}
+
 // One workgroup per NPROMA block: min/max of the field, max|d|, sum|d|, sum|ref|
-// over the active lanes of that block (validate_mod.F90:136-146, with fabs).
+// over the active lanes of that block (validate_mod.F90:136-146, with fabs);
+// the sums as double-doubles.  part[b] = {min, max, max|d|, es.hi, rs.hi, es.lo, rs.lo}.
+constexpr int kStatsPer = 7;
 template <typename real>
 __global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld, const double* __restrict__ ref,
                                                     int nlev, int klon, int nproma, long long ngptot,
                                                     long long col_offset, double* __restrict__ part) {
   const long long b = blockIdx.x;
   const long long bsize = (ngptot - b * nproma) < nproma ? (ngptot - b * nproma) : nproma;
-  double mn = __DBL_MAX__, mx = -__DBL_MAX__, me = 0.0, es = 0.0, rs = 0.0;
+  double mn = __DBL_MAX__, mx = -__DBL_MAX__, me = 0.0;
+  DD es = {0.0, 0.0}, rs = {0.0, 0.0};
   const long long per = (long long)nlev * nproma;   // 64-bit: may exceed 2^31 at large NPROMA
   for (long long e = threadIdx.x; e < per; e += blockDim.x) {
     const long long L = e / nproma, i = e - L * nproma;
@@ -52,21 +72,26 @@ __global__ void __launch_bounds__(256) stats_kernel(const real* __restrict__ fld
     const double v = (double)fld[b * per + e];
     const double r = ref[L * klon + g % klon];
     const double d = fabs(v - r);
-    mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, d); es += d; rs += fabs(r);
+    mn = fmin(mn, v); mx = fmax(mx, v); me = fmax(me, d);
+    es = dd_add(es, DD{d, 0.0});
+    rs = dd_add(rs, DD{fabs(r), 0.0});
   }
-  __shared__ double s[5][256];
-  s[0][threadIdx.x] = mn; s[1][threadIdx.x] = mx; s[2][threadIdx.x] = me; s[3][threadIdx.x] = es; s[4][threadIdx.x] = rs;
+  __shared__ double s[kStatsPer][256];
+  const int t = threadIdx.x;
+  s[0][t] = mn; s[1][t] = mx; s[2][t] = me; s[3][t] = es.hi; s[4][t] = rs.hi; s[5][t] = es.lo; s[6][t] = rs.lo;
   __syncthreads();
   for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      const int t = threadIdx.x;
+    if (t < w) {
       s[0][t] = fmin(s[0][t], s[0][t + w]); s[1][t] = fmax(s[1][t], s[1][t + w]);
-      s[2][t] = fmax(s[2][t], s[2][t + w]); s[3][t] += s[3][t + w]; s[4][t] += s[4][t + w];
+      s[2][t] = fmax(s[2][t], s[2][t + w]);
+      const DD a = dd_add(DD{s[3][t], s[5][t]}, DD{s[3][t + w], s[5][t + w]});
+      const DD c = dd_add(DD{s[4][t], s[6][t]}, DD{s[4][t + w], s[6][t + w]});
+      s[3][t] = a.hi; s[5][t] = a.lo; s[4][t] = c.hi; s[6][t] = c.lo;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0)
-    for (int q = 0; q < 5; q++) part[b * 5 + q] = s[q][0];
+  if (t == 0)
+    for (int q = 0; q < kStatsPer; q++) part[b * kStatsPer + q] = s[q][0];
 }
 
 // ---------------------------------------------------------------------------
@@ -322,10 +347,10 @@ int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* re
   HIPCHK(hipStreamSynchronize(s->stream));
   double* part = nullptr;
   double* dref = nullptr;
-  HIPCHK(hipMalloc(&part, (size_t)s->nblocks * 5 * sizeof(double)));
+  HIPCHK(hipMalloc(&part, (size_t)s->nblocks * kStatsPer * sizeof(double)));
   const size_t max_ref = (size_t)5 * (s->klev + 1) * ref->klon;
   hipError_t e = hipMalloc(&dref, max_ref * sizeof(double));
-  std::vector<double> h((size_t)s->nblocks * 5);
+  std::vector<double> h((size_t)s->nblocks * kStatsPer);
   for (int id = 0; id < CLOUDSC_NVALID && e == hipSuccess; id++) {
     int kind;
     void* const* slot = valid_slot(s, id, &kind);
@@ -343,10 +368,11 @@ int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* re
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e == hipSuccess) e = hipMemcpy(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost);
     if (e != hipSuccess) break;
-    cloudsc_stats_t t = {__DBL_MAX__, -__DBL_MAX__, 0.0, 0.0, 0.0};
-    for (int b = 0; b < s->nblocks; b++) {            // block order: deterministic
-      t.minval = fmin(t.minval, h[b * 5 + 0]); t.maxval = fmax(t.maxval, h[b * 5 + 1]);
-      t.maxerr = fmax(t.maxerr, h[b * 5 + 2]); t.errsum += h[b * 5 + 3]; t.refsum += h[b * 5 + 4];
+    cloudsc_stats_t t = {__DBL_MAX__, -__DBL_MAX__, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int b = 0; b < s->nblocks; b++) {            // double-double sums: any order gives the same double
+      const double* q = &h[(size_t)b * kStatsPer];
+      const cloudsc_stats_t pb = {q[0], q[1], q[2], q[3], q[4], q[5], q[6]};
+      cloudsc_stats_combine(&t, &pb);
     }
     stats[id] = t;
   }
@@ -354,6 +380,17 @@ int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* re
   (void)hipFree(dref);
   if (e != hipSuccess) return hip_fail(e, "validate");
   return CLOUDSC_OK;
+}
+
+void cloudsc_stats_combine(cloudsc_stats_t* acc, const cloudsc_stats_t* p) {
+  if (!acc || !p) return;
+  acc->minval = fmin(acc->minval, p->minval);
+  acc->maxval = fmax(acc->maxval, p->maxval);
+  acc->maxerr = fmax(acc->maxerr, p->maxerr);
+  const DD e = dd_add(DD{acc->errsum, acc->errsum_lo}, DD{p->errsum, p->errsum_lo});
+  const DD r = dd_add(DD{acc->refsum, acc->refsum_lo}, DD{p->refsum, p->refsum_lo});
+  acc->errsum = e.hi; acc->errsum_lo = e.lo;
+  acc->refsum = r.hi; acc->refsum_lo = r.lo;
 }
 
 int cloudsc_state_destroy(cloudsc_gpu_state_t* s) {

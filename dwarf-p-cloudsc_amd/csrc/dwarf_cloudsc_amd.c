@@ -540,14 +540,7 @@ int main(int argc, char **argv) {
     double worst = 0.0;
     for (int f = 0; f < CLOUDSC_NVALID; f++) {
       cloudsc_stats_t s = sh[0].stats[f];
-      for (int d = 1; d < nused; d++) {
-        const cloudsc_stats_t *q = &sh[d].stats[f];
-        s.minval = fmin(s.minval, q->minval);
-        s.maxval = fmax(s.maxval, q->maxval);
-        s.maxerr = fmax(s.maxerr, q->maxerr);
-        s.errsum += q->errsum;
-        s.refsum += q->refsum;
-      }
+      for (int d = 1; d < nused; d++) cloudsc_stats_combine(&s, &sh[d].stats[f]);   /* double-double sums */
       const int kind = cloudsc_io_ref_kind[f];
       const double rel = print_error(cloudsc_io_print_names[f], kind == 3 ? 1 : kind == 2 ? 3 : 2, &s, o.ngptot);
       if (rel > worst) worst = rel;

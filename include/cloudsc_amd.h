@@ -270,10 +270,22 @@ typedef struct cloudsc_reference {
   const double *field[CLOUDSC_NVALID];
 } cloudsc_reference_t;
 
-/* Per-field statistics, the inputs of ERROR_PRINT (validate_mod.F90:263-296). */
+/* Per-field statistics, the inputs of ERROR_PRINT (validate_mod.F90:263-296).
+ * The two sums are carried as double-doubles: errsum / refsum are the sums
+ * rounded to double, errsum_lo / refsum_lo what that rounding left over (all
+ * terms are non-negative, so hi + lo holds the sum to ~100 bits).  Sums of
+ * partial statistics -- NPROMA blocks on the device, shards on the host, the
+ * MPI_Reduce of validate_mod.F90:53-55 -- therefore do not depend on how the
+ * columns were partitioned: a sharded run prints the unsharded run's table to
+ * the last digit.  Combine partials with cloudsc_stats_combine. */
 typedef struct cloudsc_stats {
   double minval, maxval, maxerr, errsum, refsum;
+  double errsum_lo, refsum_lo;
 } cloudsc_stats_t;
+
+/* acc <- acc (+) part: min of mins, max of maxes and of max|d|, double-double
+ * sums.  Start from {DBL_MAX, -DBL_MAX, 0, 0, 0, 0, 0}. */
+void cloudsc_stats_combine(cloudsc_stats_t *acc, const cloudsc_stats_t *part);
 
 typedef struct cloudsc_gpu_state cloudsc_gpu_state_t;
 

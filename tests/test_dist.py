@@ -97,3 +97,47 @@ def test_combine_stats_matches_unsharded(ds):
         comb = cd.combine_stats([[h] for h in halves])[0]
         assert comb[:3] == whole[:3]
         assert comb[3] == pytest.approx(whole[3], rel=1e-12) and comb[4] == pytest.approx(whole[4], rel=1e-12)
+
+
+def test_double_double_sums_are_partition_invariant():
+    """The validation sums are double-doubles (cloudsc_stats_t), so per-block,
+    per-shard and per-rank partials combine to the same double however the
+    columns are split -- the property that makes a sharded dwarf print the
+    unsharded run's table to the last digit.  Checked against math.fsum (the
+    correctly rounded sum) for random splits of 10^5 non-negative terms."""
+    import math
+    rng = np.random.default_rng(3)
+    x = np.abs(rng.standard_normal(100000)) * 10.0 ** rng.integers(-20, 5, 100000)
+    exact = math.fsum(x)
+    for nparts in (1, 2, 3, 8, 10240):
+        cuts = np.sort(rng.choice(np.arange(1, x.size), nparts - 1, replace=False)) if nparts > 1 else []
+        parts = np.split(x, cuts)
+        partial = []
+        for p in parts:                          # each part summed element by element
+            acc = (0.0, 0.0)
+            for v in p.tolist():
+                acc = cd.dd_add(acc, (v, 0.0))
+            partial.append(acc)
+        order = rng.permutation(len(partial))    # and combined in any order
+        tot = (0.0, 0.0)
+        for i in order:
+            tot = cd.dd_add(tot, partial[i])
+        assert tot[0] == exact, nparts
+
+
+def test_stats_combine_c_abi_matches_python():
+    """cloudsc_stats_combine (libcloudsc_amd, host code: no GPU needed) is the
+    same arithmetic as cloudsc_dist.combine_stats."""
+    import ctypes as C
+    lib = ca.gpu_lib()
+    lib.cloudsc_stats_combine.argtypes = [C.POINTER(ca.Stats), C.POINTER(ca.Stats)]
+    rng = np.random.default_rng(5)
+    rows = [tuple(float(v) for v in (-rng.random(), rng.random(), rng.random(), rng.random() * 1e3,
+                                      rng.random() * 1e6, rng.random() * 1e-14, rng.random() * 1e-11))
+            for _ in range(17)]
+    acc = ca.Stats(1.7976931348623157e308, -1.7976931348623157e308, 0.0, 0.0, 0.0, 0.0, 0.0)
+    for r in rows:
+        part = ca.Stats(*r)
+        lib.cloudsc_stats_combine(C.byref(acc), C.byref(part))
+    py = cd.combine_stats([[r] for r in rows])[0]
+    assert (acc.minval, acc.maxval, acc.maxerr, acc.errsum, acc.refsum, acc.errsum_lo, acc.refsum_lo) == py
