@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--variant", choices=["kseg", "kcache", "scc", "scc-private"], default=None,
                    help="default: kseg (the persistent kernel: 2560 wave-sized units on 2 waves/SIMD without a "
                         "tail; fp64 and fp32, profiles/r02/kseg_grid_sweep.jsonl)")
+    p.add_argument("--fp32-exact-libm", action="store_true",
+                   help="fp32: exp/pow with the glibc algorithms (bit-identical to the fp32 restatement) instead of "
+                        "the default float-internal device forms")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-transfer", action="store_true",
                    help="skip the host-buffer path (H2D -> kernel -> D2H, chunked over streams), which N=1 runs "
@@ -159,6 +162,9 @@ def main():
     prec = ca.FP64 if args.precision == "fp64" else ca.FP32
     variant = {"kseg": ca.VARIANT_KSEG, "kcache": ca.VARIANT_KCACHE, "scc": ca.VARIANT_SCC,
                "scc-private": ca.VARIANT_SCC_PRIVATE}[args.variant]
+    kind = variant
+    if args.fp32_exact_libm:
+        variant |= ca.FP32_EXACT_LIBM
     ds = ca.load_dataset()
     # one GPU per local rank (ranks beyond the device count share devices, e.g.
     # a 2-rank rehearsal on a 1-GPU box)
@@ -220,8 +226,10 @@ def main():
         "config": {"workload": "CLOUDSC %s, NGPTOT=%d per GPU, KLEV=%d, NPROMA=%d, %s" % (
             {ca.VARIANT_KSEG: "SCC-k-caching (persistent, level-segmented)",
              ca.VARIANT_KCACHE: "SCC-k-caching", ca.VARIANT_SCC: "SCC (HBM temporaries)",
-             ca.VARIANT_SCC_PRIVATE: "SCC (per-thread private-array temporaries)"}[variant],
+             ca.VARIANT_SCC_PRIVATE: "SCC (per-thread private-array temporaries)"}[kind],
             args.ngptot, ds.klev, args.nproma, args.precision),
+            "libm": "reference CPU build's exp/pow (glibc algorithms)" if prec == ca.FP64 or args.fp32_exact_libm
+                    else "float-internal expf/powf (hardware exp2/log2, exact argument reduction)",
             "ngptot_per_gpu": args.ngptot, "ngptot_total": total_cols, "klev": ds.klev,
             "nproma": args.nproma, "variant": args.variant, "parallelism": "columns sharded, %d GPU(s)" % world},
         "kernel_ms": round(k_avg_ms, 4),

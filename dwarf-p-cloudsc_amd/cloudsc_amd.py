@@ -409,11 +409,14 @@ def gpu_lib(path: Optional[str] = None):
     lib.cloudsc_debug_set_kseg_schedule.argtypes = [C.c_int, C.c_int]
     lib.cloudsc_debug_host_pipeline_mapping.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     lib.cloudsc_debug_host_pinned.argtypes = [C.c_void_p, C.c_longlong]
+    lib.cloudsc_debug_fp32_libm.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_longlong]
     _lib = lib
     return lib
 
 
 EHANDOFF = -7
+# option bit of a variant argument: fp32 exp/pow with the glibc algorithms (bit-identical to the fp32 restatement)
+FP32_EXACT_LIBM = 0x100
 
 
 def kseg_schedule(nseg: int = 0, grid: int = 0) -> None:

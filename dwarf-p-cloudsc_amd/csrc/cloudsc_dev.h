@@ -61,6 +61,23 @@ struct DevParams {
   int nssopt, ncldtop, laericesed, laericeauto;
 };
 
+// The parameter block as the kernels see it: the same memory, with the choice
+// of the single-precision exp/pow forms carried in the type (FAST = the
+// float-internal device forms below; false = the reference CPU build's
+// algorithms).  The phase functions take the block as `const P& c` and pass it
+// to cl_exp / cl_pow, so the choice costs nothing at run time.  fp64 is always
+// the reference's algorithms (FAST is only instantiated for float).
+template <typename real, bool FAST>
+struct DevParamsT : DevParams<real> {};
+template <typename P>
+struct LibmFast {
+  static constexpr bool value = false;
+};
+template <>
+struct LibmFast<DevParamsT<float, true>> {
+  static constexpr bool value = true;
+};
+
 // The phase functions of the physics (cloudsc_kcache.h) and the helpers below
 // compile for the device (the kernels) and for the host (cloudsc_cpu_run,
 // cloudsc_cpu.hip: the same source as the explicitly selected CPU variant).
@@ -255,6 +272,45 @@ inline float cl_powr_host(float x, float y) {
 }
 inline double cl_exp_host(double x) { return cloudsc_libm::exp_split(x, cloudsc_libm::HostTabs{}, HostLibmCold{}); }
 inline float cl_exp_host(float x) { return cloudsc_libm::expf_split(x, cloudsc_libm::HostTabsF{}, HostLibmCold{}); }
+// Single precision, float-internal (CLOUDSC_FP32 default; the glibc forms
+// above with CLOUDSC_FP32_EXACT_LIBM).  expf: x*log2(e) as an exact
+// head + tail (Cody-Waite with an fma), the hardware 2^f (v_exp_f32, 1 ulp on
+// |f| <= 1/2) and ldexp.  powf: log2 of the mantissa in [1/2, 1) by the
+// hardware log2 (v_log_f32) plus the exponent, y*log2(x) as a float-float
+// (products split with fma, TwoSum), then the same exp2 + ldexp.  Every
+// operation is float (2-cycle issue on gfx950, against 4 for the double
+// internals of glibc's forms); the arguments outside the hot range go to the
+// complete glibc functions (cold).  Accuracy: tests/test_gpu_parity.py
+// (test_fp32_fast_libm_ulp) measures <= 2 ulp against the glibc forms over the
+// argument ranges CLOUDSC uses.
+__device__ __forceinline__ float cl_expf_fast(float x) {
+  if (__builtin_expect(!(__builtin_fabsf(x) < 88.0f), 0)) return cl_expf_cold(x);
+  const float kL2e = 0x1.715476p+0f, kL2eLo = 0x1.4ae0bep-26f;   // log2(e) = kL2e + kL2eLo (+ O(2^-50))
+  const float ph = x * kL2e;
+  float pl = __builtin_fmaf(x, kL2e, -ph);                         // exact: x*kL2e = ph + pl
+  pl = __builtin_fmaf(x, kL2eLo, pl);
+  const float e = __builtin_rintf(ph);
+  const float f = (ph - e) + pl;                                    // |f| <= 1/2 + tiny
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)e);
+}
+__device__ __forceinline__ float cl_powf_fast(float x, float y) {
+  const uint32_t ix = __builtin_bit_cast(uint32_t, x), iy = __builtin_bit_cast(uint32_t, y);
+  // hot range: x a positive normal number, y finite and non-zero (else the complete function)
+  if (__builtin_expect(ix - 0x00800000u >= 0x7f800000u - 0x00800000u || 2 * iy - 1 >= 2u * 0x7f800000u - 1, 0))
+    return cl_powf_cold(x, y);
+  const float m = __builtin_amdgcn_frexp_mantf(x);                 // x = m * 2^E, m in [1/2, 1)
+  const float E = (float)__builtin_amdgcn_frexp_expf(x);
+  const float l = __builtin_amdgcn_logf(m);                         // log2(m), in [-1, 0)
+  const float a = y * E, a_lo = __builtin_fmaf(y, E, -a);          // y*E = a + a_lo exactly
+  const float b = y * l, b_lo = __builtin_fmaf(y, l, -b);          // y*l = b + b_lo exactly
+  const float hi = a + b, bb = hi - a;
+  const float lo = ((a - (hi - bb)) + (b - bb)) + (a_lo + b_lo);   // TwoSum error + the product tails
+  if (__builtin_expect(!(__builtin_fabsf(hi) < 126.0f), 0)) return cl_powf_cold(x, y);
+  const float k = __builtin_rintf(hi);
+  const float f = (hi - k) + lo;
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)k);
+}
+
 template <typename real>
 CLOUDSC_HD real cl_pow(real x, real y) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -270,6 +326,21 @@ CLOUDSC_HD real cl_exp(real x) {
 #else
   return cl_exp_host(x);
 #endif
+}
+// the physics' exp / pow: the form is chosen by the parameter block's type
+template <typename real, typename P>
+CLOUDSC_HD real cl_exp(const P&, typename std::common_type<real>::type x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) return cl_expf_fast(x);
+#endif
+  return cl_exp<real>(x);
+}
+template <typename real, typename P>
+CLOUDSC_HD real cl_pow(const P&, typename std::common_type<real>::type x, typename std::common_type<real>::type y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) return cl_powf_fast(x, y);
+#endif
+  return cl_pow<real>(x, y);
 }
 
 // Division.  The IEEE sequence hipcc emits for a / b is
@@ -394,9 +465,9 @@ CLOUDSC_HD real foealfa(const P& c, real t) {
   return fmin(R(1.0), x * x);            // pow(x,2) == x*x (both rounded once)
 }
 template <typename real, typename P>
-CLOUDSC_HD real exp_liq(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3les * (t - c.rtt), t - c.r4les)); }
+CLOUDSC_HD real exp_liq(const P& c, real t) { return cl_exp<real>(c, cl_div<real>(c.r3les * (t - c.rtt), t - c.r4les)); }
 template <typename real, typename P>
-CLOUDSC_HD real exp_ice(const P& c, real t) { return cl_exp<real>(cl_div<real>(c.r3ies * (t - c.rtt), t - c.r4ies)); }
+CLOUDSC_HD real exp_ice(const P& c, real t) { return cl_exp<real>(c, cl_div<real>(c.r3ies * (t - c.rtt), t - c.r4ies)); }
 
 // alfa*R5ALVCP/(T-R4LES)^2 + (1-alfa)*R5ALSCP/(T-R4IES)^2 (cloudsc_c.c:1166,1220)
 template <typename real, typename P>

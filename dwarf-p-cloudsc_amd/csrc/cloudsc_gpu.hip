@@ -164,10 +164,11 @@ KArgs<real> make_args(const cloudsc_fields_t* f, int ngptot, int nproma, int kle
   return a;
 }
 
-// the launch's parameter block, as a constant-address-space pointer (scalar loads)
-template <typename real>
-__device__ __forceinline__ cptr<DevParams<real>> params_of(cptr<KArgs<real>> ka) {
-  return (cptr<DevParams<real>>)((const KArgs<real>*)ka)->par;
+// the launch's parameter block, as a constant-address-space pointer (scalar
+// loads), typed with the kernel's choice of single-precision exp/pow forms
+template <typename real, bool FAST>
+__device__ __forceinline__ cptr<DevParamsT<real, FAST>> params_of(cptr<KArgs<real>> ka) {
+  return (cptr<DevParamsT<real, FAST>>)((const KArgs<real>*)ka)->par;
 }
 
 }  // namespace
@@ -175,33 +176,35 @@ __device__ __forceinline__ cptr<DevParams<real>> params_of(cptr<KArgs<real>> ka)
 // Kernel entry points.  The KArgs struct is the first explicit kernel argument,
 // i.e. it sits at offset 0 of the kernarg segment; the bodies read it (and the
 // parameter block it points at) through constant-address-space pointers.
-template <typename real, int WAVES, int PF, bool AER, bool LDSC>
+// FAST: fp32 exp/pow in their float-internal device forms (the CLOUDSC_FP32
+// default); false: the reference CPU build's algorithms (always for fp64).
+template <typename real, int WAVES, int PF, bool AER, bool LDSC, bool FAST = false>
 __global__ void __launch_bounds__(256, WAVES) kcache_entry(const KArgs<real> a) {
   (void)a;
   libm_tables_to_lds<real>();
   const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
-  cloudsc_kcache_body<real, PF, AER, LDSC>(ka, params_of<real>(ka));
+  cloudsc_kcache_body<real, PF, AER, LDSC>(ka, params_of<real, FAST>(ka));
 }
-template <typename real, int WAVES, int PF, bool AER, bool LDSC>
+template <typename real, int WAVES, int PF, bool AER, bool LDSC, bool FAST = false>
 __global__ void __launch_bounds__(256, WAVES) kseg_entry(const KArgs<real> a, const PersistArgs<real> pa) {
   (void)a;
   libm_tables_to_lds<real>();
   const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
-  cloudsc_kcache_persistent_body<real, PF, AER, LDSC>(ka, params_of<real>(ka), pa);
+  cloudsc_kcache_persistent_body<real, PF, AER, LDSC>(ka, params_of<real, FAST>(ka), pa);
 }
-template <typename real, bool AER>
+template <typename real, bool AER, bool FAST = false>
 __global__ void __launch_bounds__(256) scc_entry(const KArgs<real> a, const SccScratch<real> s) {
   (void)a;
   libm_tables_to_lds<real>();
   const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
-  cloudsc_scc_body<real, AER>(ka, s, params_of<real>(ka));
+  cloudsc_scc_body<real, AER>(ka, s, params_of<real, FAST>(ka));
 }
-template <typename real, bool AER>
+template <typename real, bool AER, bool FAST = false>
 __global__ void __launch_bounds__(256) scc_private_entry(const KArgs<real> a) {
   (void)a;
   libm_tables_to_lds<real>();
   const cptr<KArgs<real>> ka = (cptr<KArgs<real>>)__builtin_amdgcn_kernarg_segment_ptr();
-  cloudsc_scc_private_body<real, AER>(ka, params_of<real>(ka));
+  cloudsc_scc_private_body<real, AER>(ka, params_of<real, FAST>(ka));
 }
 
 // ---------------------------------------------------------------------------
@@ -229,7 +232,7 @@ template <> struct DefaultCfg<float> { static constexpr int code = 21, waves = 2
 // code: [1]<waves><pf> -- leading 1 = carried state in LDS
 #define CLOUDSC_FOR_EACH_CFG(X) \
   X(10, 1, 0, false) X(11, 1, 1, false) X(20, 2, 0, false) X(21, 2, 1, false) X(30, 3, 0, false) \
-  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) \
+  X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) X(23, 2, 3, false) \
   X(122, 2, 2, true) X(130, 3, 0, true) X(132, 3, 2, true) X(22, 2, 2, false) X(131, 3, 1, true) X(140, 4, 0, true)
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -247,13 +250,13 @@ void launch_physics(void (*kern)(Args...), dim3 grid, dim3 block, size_t lds, hi
   else hipLaunchKernelGGL(kern, grid, block, lds, st, args...);
 }
 
-template <typename real, bool AER>
+template <typename real, bool AER, bool FAST>
 int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma, const LaunchEvents* ev) {
 #ifdef CLOUDSC_DEBUG_KNOBS
   switch (env_int("CLOUDSC_KCACHE_CFG", DefaultCfg<real>::code)) {
 #define X(code, w, pf, ldsc)                                                                                 \
   case code:                                                                                                 \
-    launch_physics(kcache_entry<real, w, pf, AER, ldsc>, dim3(nblocks), dim3(nproma),                       \
+    launch_physics(kcache_entry<real, w, pf, AER, ldsc, FAST>, dim3(nblocks), dim3(nproma),                 \
                    ldsc ? carry_lds_bytes<real>(nproma) : 0, st, ev, a);                                     \
     return CLOUDSC_OK;
     CLOUDSC_FOR_EACH_CFG(X)
@@ -261,7 +264,7 @@ int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma,
     default: return CLOUDSC_EINVAL;
   }
 #else
-  launch_physics(kcache_entry<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>, dim3(nblocks),
+  launch_physics(kcache_entry<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false, FAST>, dim3(nblocks),
                  dim3(nproma), 0, st, ev, a);
   return CLOUDSC_OK;
 #endif
@@ -334,11 +337,11 @@ __global__ void __launch_bounds__(256) kseg_prepare_kernel(unsigned* ws, int nfl
 
 namespace {
 
-template <typename real, int WAVES, int PF, bool AER, bool LDSC>
+template <typename real, int WAVES, int PF, bool AER, bool LDSC, bool FAST>
 int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
                     int* grid_out, const LaunchEvents* ev) {
   const int nseg = pa.nseg;
-  auto kern = kseg_entry<real, WAVES, PF, AER, LDSC>;
+  auto kern = kseg_entry<real, WAVES, PF, AER, LDSC, FAST>;
   const int wg = kseg_wg(nproma);
   const size_t lds = LDSC ? carry_lds_bytes<real>(wg) : 0;
   // Waves per SIMD: as many as fit, but no more than whole rounds of the work
@@ -379,26 +382,26 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   return CLOUDSC_OK;
 }
 
-template <typename real, bool AER>
+template <typename real, bool AER, bool FAST>
 int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& pa, int nproma, int nitems,
                 int* grid_out, const LaunchEvents* ev) {
 #ifdef CLOUDSC_DEBUG_KNOBS
   switch (env_int("CLOUDSC_KCACHE_CFG", DefaultCfg<real>::code)) {
 #define X(code, w, pf, ldsc) \
-  case code: return launch_kseg_cfg<real, w, pf, AER, ldsc>(st, a, pa, nproma, nitems, grid_out, ev);
+  case code: return launch_kseg_cfg<real, w, pf, AER, ldsc, FAST>(st, a, pa, nproma, nitems, grid_out, ev);
     CLOUDSC_FOR_EACH_CFG(X)
 #undef X
     default: return CLOUDSC_EINVAL;
   }
 #else
-  return launch_kseg_cfg<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false>(st, a, pa, nproma, nitems,
+  return launch_kseg_cfg<real, DefaultCfg<real>::waves, DefaultCfg<real>::pf, AER, false, FAST>(st, a, pa, nproma, nitems,
                                                                                         grid_out, ev);
 #endif
 }
 
-template <typename real>
-int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
-           void* scratch, const void* plude_in, const ParamSet& ps, KsegEpoch* ep, const LaunchEvents* ev) {
+template <typename real, bool FAST>
+int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
+             void* scratch, const void* plude_in, const ParamSet& ps, KsegEpoch* ep, const LaunchEvents* ev) {
   KArgs<real> a = make_args<real>(f, ngptot, nproma, klev, ps);
   if (plude_in) a.plude_in = (const real*)plude_in;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
@@ -406,7 +409,8 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
   if (aer && (!f->pre_ice || !f->picrit_aer || !f->pnice)) return CLOUDSC_EINVAL;
   int rc = CLOUDSC_OK;
   if (variant == CLOUDSC_VARIANT_KCACHE) {
-    rc = aer ? launch_kcache<real, true>(st, a, nblocks, nproma, ev) : launch_kcache<real, false>(st, a, nblocks, nproma, ev);
+    rc = aer ? launch_kcache<real, true, FAST>(st, a, nblocks, nproma, ev)
+             : launch_kcache<real, false, FAST>(st, a, nblocks, nproma, ev);
   } else if (variant == CLOUDSC_VARIANT_KSEG) {
     if (!scratch) return CLOUDSC_EINVAL;
     PersistArgs<real> pa;
@@ -455,8 +459,8 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
     pa.base = zero_ws ? 0u : ep->base;
     pa.stamp = zero_ws ? 0u : ep->stamp;
     int grid = 0;
-    rc = aer ? launch_kseg<real, true>(st, a, pa, nproma, pa.nitems, &grid, ev)
-             : launch_kseg<real, false>(st, a, pa, nproma, pa.nitems, &grid, ev);
+    rc = aer ? launch_kseg<real, true, FAST>(st, a, pa, nproma, pa.nitems, &grid, ev)
+             : launch_kseg<real, false, FAST>(st, a, pa, nproma, pa.nitems, &grid, ev);
     if (rc) return rc;
     HIPCHK(hipGetLastError());
     if (ep) {   // the next launch on this workspace continues where this one ends
@@ -466,17 +470,29 @@ int launch(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, i
     }
   } else if (variant == CLOUDSC_VARIANT_SCC_PRIVATE) {
     if (klev > kPrivKlev) return CLOUDSC_EINVAL;    // the private arrays are sized at compile time
-    if (aer) launch_physics(scc_private_entry<real, true>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
-    else launch_physics(scc_private_entry<real, false>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
+    if (aer) launch_physics(scc_private_entry<real, true, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
+    else launch_physics(scc_private_entry<real, false, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
   } else {
     if (!scratch) return CLOUDSC_EINVAL;
     SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
-    if (aer) launch_physics(scc_entry<real, true>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
-    else launch_physics(scc_entry<real, false>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
+    if (aer) launch_physics(scc_entry<real, true, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
+    else launch_physics(scc_entry<real, false, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
   }
   if (rc) return rc;
   HIPCHK(hipGetLastError());
   return CLOUDSC_OK;
+}
+
+// fp32 runs the float-internal exp/pow unless the caller asks for the
+// reference CPU build's forms (CLOUDSC_FP32_EXACT_LIBM); fp64 has only those
+template <typename real>
+int launch(hipStream_t st, int variant, bool exact_libm, const cloudsc_fields_t* f, int ngptot, int nproma,
+           int klev, void* scratch, const void* plude_in, const ParamSet& ps, KsegEpoch* ep, const LaunchEvents* ev) {
+  if constexpr (std::is_same<real, float>::value) {
+    if (!exact_libm) return launch_v<real, true>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, ps, ep, ev);
+  }
+  (void)exact_libm;
+  return launch_v<real, false>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, ps, ep, ev);
 }
 
 }  // namespace
@@ -511,6 +527,7 @@ int cloudsc_gpu_init(int device, const cloudsc_params_t* params) {
 
 long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev) {
   if (ngptot <= 0 || nproma <= 0 || klev < 2) return -1;
+  variant = variant_kind(variant);
   if (variant == CLOUDSC_VARIANT_KCACHE || variant == CLOUDSC_VARIANT_SCC_PRIVATE) return 0;
   if (precision != CLOUDSC_FP64 && precision != CLOUDSC_FP32) return -1;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
@@ -526,6 +543,8 @@ long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int 
 
 namespace cloudsc_impl {
 int validate_run_args(int device, int precision, int variant, int ngptot, int nproma, int klev) {
+  if (variant & ~(0xff | CLOUDSC_FP32_EXACT_LIBM)) return CLOUDSC_EINVAL;
+  variant = variant_kind(variant);
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CLOUDSC_ENODEV;
   if (device < 0 || device >= n || device >= kMaxDevices) return CLOUDSC_ENODEV;
@@ -546,6 +565,8 @@ int validate_run_args(int device, int precision, int variant, int ngptot, int np
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
                  const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps,
                  KsegEpoch* ep, const LaunchEvents* lev) {
+  const bool exact_libm = (variant & CLOUDSC_FP32_EXACT_LIBM) != 0;
+  variant = variant_kind(variant);
   int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
   if (rc) return rc;
   if (!ps) ps = device_default_params(device);
@@ -554,8 +575,9 @@ int gpu_run_impl(int device, void* stream, int precision, int variant, int ngpto
   if (!f || !fields_complete(f)) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
-  return precision == CLOUDSC_FP64 ? launch<double>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev)
-                                   : launch<float>(st, variant, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev);
+  return precision == CLOUDSC_FP64
+             ? launch<double>(st, variant, exact_libm, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev)
+             : launch<float>(st, variant, exact_libm, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev);
 }
 
 int kseg_check(int device, void* stream, void* scratch) {
@@ -585,7 +607,7 @@ int cloudsc_gpu_run(int device, void* stream, int precision, int variant, int ng
 int cloudsc_gpu_check(int device, void* stream, int variant, void* scratch) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CLOUDSC_ENODEV;
-  if (variant != CLOUDSC_VARIANT_KSEG) {
+  if (variant_kind(variant) != CLOUDSC_VARIANT_KSEG) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamSynchronize((hipStream_t)stream));
     return CLOUDSC_OK;
@@ -631,6 +653,46 @@ int cloudsc_kseg_trace(unsigned long long* host, int nitems) {
   return CLOUDSC_OK;
 }
 #endif
+
+// Diagnostic: the single-precision exp/pow forms of the kernels on the device,
+// element-wise (tests/test_gpu_parity.py measures their ulp distance).
+__global__ void __launch_bounds__(256) fp32_libm_kernel(int which, const float* x, const float* y, float* out,
+                                                        long long n) {
+  libm_tables_to_lds<float>();
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float r;
+  switch (which) {
+    case 0: r = cl_expf_fast(x[i]); break;
+    case 1: r = cl_powf_fast(x[i], y[i]); break;
+    case 2: r = cl_exp_impl(x[i]); break;
+    default: r = cl_powr(x[i], y[i]); break;
+  }
+  out[i] = r;
+}
+
+int cloudsc_debug_fp32_libm(int device, int which, const float* x, const float* y, float* out, long long n) {
+  if (which < 0 || which > 3 || !x || !out || n <= 0 || ((which & 1) && !y)) return CLOUDSC_EINVAL;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return CLOUDSC_ENODEV;
+  HIPCHK(hipSetDevice(device));
+  float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  const size_t bytes = (size_t)n * sizeof(float);
+  hipError_t e = hipMalloc(&dx, bytes);
+  if (e == hipSuccess) e = hipMalloc(&dy, bytes);
+  if (e == hipSuccess) e = hipMalloc(&dout, bytes);
+  if (e == hipSuccess) e = hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dy, y ? y : x, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(fp32_libm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, which, dx, dy,
+                       dout, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(dx); (void)hipFree(dy); (void)hipFree(dout);
+  if (e != hipSuccess) return hip_fail(e, "fp32 libm diagnostic");
+  return CLOUDSC_OK;
+}
 
 long long cloudsc_abi_sizeof(int which) {
   switch (which) {

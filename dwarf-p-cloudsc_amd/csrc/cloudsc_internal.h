@@ -55,6 +55,8 @@ struct LaunchEvents {
 int gpu_run_impl(int device, void* stream, int precision, int variant, int ngptot, int nproma, int klev,
                  const cloudsc_fields_t* f, void* scratch, const void* plude_in, const ParamSet* ps,
                  KsegEpoch* ep = nullptr, const LaunchEvents* lev = nullptr);
+// the kernel variant of a `variant` argument without its option bits (CLOUDSC_FP32_EXACT_LIBM)
+inline int variant_kind(int variant) { return variant & 0xff; }
 // waits for `stream` and returns CLOUDSC_EHANDOFF if the last KSEG launch on
 // `scratch` counted a timed-out segment hand-off
 int kseg_check(int device, void* stream, void* scratch);

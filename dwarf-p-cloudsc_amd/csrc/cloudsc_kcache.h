@@ -27,7 +27,7 @@
 // fp64 output is the reference kernel's, bit for bit.
 #pragma once
 #include "cloudsc_dev.h"
-#define CLOUDSC_PARAMS_HERE const DevParams<real>& c = *(const DevParams<real>*)launder_uniform(cpar)
+#define CLOUDSC_PARAMS_HERE const PT& c = *(const PT*)launder_uniform(cpar)
 
 namespace cloudsc {
 
@@ -81,6 +81,46 @@ struct LevelIn {
   real pclv[4], ttcld[4];
   real pre_ice, picrit_aer, pnice;      // aerosol inputs, loaded only under LAERICESED/LAERICEAUTO
 };
+
+// PF 3: the inputs section 1 and the start of section 3 consume first
+// (init_level, the saturation values), prefetched for level k+1 in the middle
+// of level k; the rest is loaded at the top of its own level.
+template <typename real>
+struct EarlyIn {
+  real pt, pq, ttt, ttq, tta, pa, pap;
+  real pclv[4], ttcld[4];
+};
+template <typename real>
+CLOUDSC_HD void load_early(EarlyIn<real>& E, const KArgs<real>& A, size_t u2, size_t u3, int k, int klev,
+                           int nproma, unsigned lo) {
+  const size_t i = u2 + (size_t)k * nproma;
+  E.pt = ldg1(A.pt, i, lo); E.pq = ldg1(A.pq, i, lo); E.ttt = ldg1(A.ttt, i, lo); E.ttq = ldg1(A.ttq, i, lo);
+  E.tta = ldg1(A.tta, i, lo); E.pa = ldg1(A.pa, i, lo); E.pap = ldg1(A.pap, i, lo);
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const size_t j = u3 + ((size_t)m * klev + k) * nproma;
+    E.pclv[m] = ldg1(A.pclv, j, lo);
+    E.ttcld[m] = ldg1(A.ttcld, j, lo);
+  }
+}
+template <typename real, bool AER>
+CLOUDSC_HD void load_late(LevelIn<real>& L, const KArgs<real>& A, size_t u2, int k, int nproma, unsigned lo) {
+  const size_t i = u2 + (size_t)k * nproma;
+  L.plude = ldg1(A.plude_in, i, lo); L.pvfl = ldg1(A.pvfl, i, lo); L.pvfi = ldg1(A.pvfi, i, lo);
+  L.phrsw = ldg1(A.phrsw, i, lo); L.phrlw = ldg1(A.phrlw, i, lo); L.pvervel = ldg1(A.pvervel, i, lo);
+  L.psnde = ldg1(A.psnde, i, lo); L.psupsat = ldg1(A.psupsat, i, lo);
+  if (AER) {
+    L.pre_ice = ldg1(A.pre_ice, i, lo); L.picrit_aer = ldg1(A.picrit_aer, i, lo); L.pnice = ldg1(A.pnice, i, lo);
+  } else {
+    L.pre_ice = R(0.0); L.picrit_aer = R(1.0); L.pnice = R(1.0);
+  }
+}
+template <typename real>
+CLOUDSC_HD void take_early(LevelIn<real>& L, const EarlyIn<real>& E) {
+  L.pt = E.pt; L.pq = E.pq; L.ttt = E.ttt; L.ttq = E.ttq; L.tta = E.tta; L.pa = E.pa; L.pap = E.pap;
+#pragma unroll
+  for (int m = 0; m < 4; m++) { L.pclv[m] = E.pclv[m]; L.ttcld[m] = E.ttcld[m]; }
+}
 
 // Values of the neighbouring levels the physics of level k reads.
 template <typename real>
@@ -246,11 +286,17 @@ CLOUDSC_HD void init_level(const P& c, const LevelIn<real>& in, LevelState<real>
 }
 
 // ===== 3.-6. physics of one level ncldtop <= k (cloudsc_c.c:732-2508) =====
-template <typename real, typename P, typename CS>
+// Nothing to do at the middle of a level (the default hook of physics_level).
+struct NoMidHook {
+  CLOUDSC_HD void operator()() const {}
+};
+
+template <typename real, typename P, typename CS, typename Mid = NoMidHook>
 CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
                                               const int ncldtop0, const LevelIn<real>& in,
                                               const Neighbors<real>& nb, const ColConst<real>& cc,
-                                              LevelState<real>& ls, CS& cs, PhysOut<real>& po) {
+                                              LevelState<real>& ls, CS& cs, PhysOut<real>& po,
+                                              const Mid& mid = Mid{}) {
   const real zepsilon = R(100.0) * (sizeof(real) == 8 ? (real)__DBL_EPSILON__ : (real)__FLT_EPSILON__);
   const real zepsec = R(1.0e-14);
   const real ztw1 = R(1329.31000000000), ztw2 = R(0.00746150000000000), ztw3 = R(85000.0000000000);
@@ -532,12 +578,12 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
       const real zvpice = cl_div_known(((c.r2es * e_ice) * c.rv), c.rd, c.rd_rcp);
       const real zvpliq = zvpice * zfokoop;
-      const real zicenuclei = R(1000.0) * cl_exp<real>(cl_div((R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
+      const real zicenuclei = R(1000.0) * cl_exp<real>(c, cl_div((R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
       const real zadd = cl_div((c.rlstt * (cl_div(c.rlstt, (c.rv * ztp1)) - R(1.0))), (R(0.024) * ztp1));
       const real zbdd = cl_div(((c.rv * ztp1) * pap_k), (R(2.21) * zvpice));
-      const real zcvds = cl_div(((R(7.8) * cl_pow<real>(cl_div(zicenuclei, zrho), R(0.666))) * (zvpliq - zvpice)), ((R(8.87) * (zadd + zbdd)) * zvpice));
+      const real zcvds = cl_div(((R(7.8) * cl_pow<real>(c, cl_div(zicenuclei, zrho), R(0.666))) * (zvpliq - zvpice)), ((R(8.87) * (zadd + zbdd)) * zvpice));
       const real zice0 = fmax(zicecld, cl_div((zicenuclei * c.riceinit), zrho));
-      const real zinew = cl_pow<real>((R(0.666) * zcvds) * c.ptsphy + cl_pow<real>(zice0, R(0.666)), R(1.5));
+      const real zinew = cl_pow<real>(c, (R(0.666) * zcvds) * c.ptsphy + cl_pow<real>(c, zice0, R(0.666)), R(1.5));
       real zdepos = fmax(za * (zinew - zice0), R(0.0));
       zdepos = fmin(zdepos, zqxfg[QL]);
       const real zinfactor = fmin(cl_div_lit(zicenuclei, R(15000.0)), R(1.0));
@@ -579,23 +625,23 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     const bool cold = ztp1 <= c.rtt;
     // 4.3a autoconversion to snow (:1616-1637)
     if (cold && zicecld > zepsec) {
-      real zzco = c.zzco_snow * cl_exp<real>(c.rsnowlin2 * (ztp1 - c.rtt));
+      real zzco = c.zzco_snow * cl_exp<real>(c, c.rsnowlin2 * (ztp1 - c.rtt));
       real zlcrit = sval(c.rlcritsnow);
       if (c.laericeauto) {
         zlcrit = in.picrit_aer;
-        zzco = zzco * cl_pow<real>(cl_div(c.rnice, in.pnice), R(0.333));
+        zzco = zzco * cl_pow<real>(c, cl_div(c.rnice, in.pnice), R(0.333));
       }
       const real r = cl_div(zicecld, zlcrit);
-      sb_is = sb_is + zzco * (R(1.0) - cl_exp<real>(-(r * r)));
+      sb_is = sb_is + zzco * (R(1.0) - cl_exp<real>(c, -(r * r)));
     }
     // 4.3b warm rain, Khairoutdinov and Kogan 2000 (:1644-1761)
     if (zliqcld > zepsec) {
       real zrainaut = R(0.0), zrainacc = R(0.0);
       if (zliqcld > cc.kk_lcrit) {
-        zrainaut = ((((R(1.5) * za) * c.ptsphy) * c.rcl_kkaau) * cl_pow<real>(zliqcld, c.rcl_kkbauq)) * cc.kk_pow;
+        zrainaut = ((((R(1.5) * za) * c.ptsphy) * c.rcl_kkaau) * cl_pow<real>(c, zliqcld, c.rcl_kkbauq)) * cc.kk_pow;
         zrainaut = fmin(zrainaut, zqxfg[QL]);
         if (zrainaut < zepsec) zrainaut = R(0.0);
-        zrainacc = (((R(2.0) * za) * c.ptsphy) * c.rcl_kkaac) * cl_pow<real>(zliqcld * zraincld, c.rcl_kkbac);
+        zrainacc = (((R(2.0) * za) * c.ptsphy) * c.rcl_kkaac) * cl_pow<real>(c, zliqcld * zraincld, c.rcl_kkbac);
         zrainacc = fmin(zrainacc, zqxfg[QL]);
         if (zrainacc < zepsec) zrainacc = R(0.0);
       }
@@ -607,9 +653,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
     // riming of snow by cloud water (:1768-1808)
     if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) {
-      const real zfallcorr = cl_pow<real>(cl_div(c.rdensref, zrho), R(0.4));
+      const real zfallcorr = cl_pow<real>(c, cl_div(c.rdensref, zrho), R(0.4));
       real zsnowrime = ((((R(0.3) * cs.zcovptot) * c.ptsphy) * c.rcl_const7s) * zfallcorr) *
-                       cl_pow<real>((zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
+                       cl_pow<real>(c, (zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
       zsnowrime = fmin(zsnowrime, R(1.0));
       sb_ls = sb_ls + zsnowrime;
     }
@@ -646,9 +692,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       if (ztp1 < c.rtt) {
         real zfrzmax;
         if (cs.rainfrac > R(0.8)) {
-          const real zlambda = cl_pow<real>(cl_div(c.rcl_fac1, (zrho * zqx[QR])), c.rcl_fac2);
+          const real zlambda = cl_pow<real>(c, cl_div(c.rcl_fac1, (zrho * zqx[QR])), c.rcl_fac2);
           const real ztemp = c.rcl_fzrab * (ztp1 - c.rtt);
-          const real zfrz = ((c.ptsphy * (cl_div(c.rcl_const5r, zrho))) * (cl_exp<real>(ztemp) - R(1.0))) * cl_pow<real>(zlambda, c.rcl_const6r);
+          const real zfrz = ((c.ptsphy * (cl_div(c.rcl_const5r, zrho))) * (cl_exp<real>(c, ztemp) - R(1.0))) * cl_pow<real>(c, zlambda, c.rcl_const6r);
           zfrzmax = fmax(zfrz, R(0.0));
         } else {
           const real zcons1 = fabs(cl_div_known((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))), c.rtaumel, c.rtaumel_rcp));
@@ -683,14 +729,14 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       const real zqe = fmax(R(0.0), fmin(zqx[QV], zqsliq));
       if (zqe < zzrh * zqsliq) {
         const real zpreclr = cl_div(zqxfg[QR], cs.zcovptot);
-        const real zfallcorr = cl_pow<real>(cl_div(c.rdensref, zrho), R(0.4));
+        const real zfallcorr = cl_pow<real>(c, cl_div(c.rdensref, zrho), R(0.4));
         const real zesatliq = c.rv_rd * (c.r2es * e_liq);
-        const real zlambda = cl_pow<real>(cl_div(c.rcl_fac1, (zrho * zpreclr)), c.rcl_fac2);
-        const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * cl_pow<real>(ztp1, R(3.0))) * pap_k;
-        const real zcorr2 = cl_div((cl_pow<real>(cl_div_lit(ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
+        const real zlambda = cl_pow<real>(c, cl_div(c.rcl_fac1, (zrho * zpreclr)), c.rcl_fac2);
+        const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * cl_pow<real>(c, ztp1, R(3.0))) * pap_k;
+        const real zcorr2 = cl_div((cl_pow<real>(c, cl_div_lit(ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
         const real zsubsat = fmax(zzrh * zqsliq - zqe, R(0.0));
         const real zbeta = ((((cl_div(R(0.5), zqsliq)) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (cl_div(zcorr2, zevap_denom)) *
-                           (cl_div(R(0.78), cl_pow<real>(zlambda, c.rcl_const4r)) + cl_div((c.rcl_const2r * sqrt(zrho * zfallcorr)), (sqrt(zcorr2) * cl_pow<real>(zlambda, c.rcl_const3r))));
+                           (cl_div(R(0.78), cl_pow<real>(c, zlambda, c.rcl_const4r)) + cl_div((c.rcl_const2r * sqrt(zrho * zfallcorr)), (sqrt(zcorr2) * cl_pow<real>(c, zlambda, c.rcl_const3r))));
         const real zdenom = R(1.0) + zbeta * c.ptsphy;
         const real zdpevap = cl_div((((zcovpclr * zbeta) * c.ptsphy) * zsubsat), zdenom);
         const real zevap = fmin(zdpevap, zqxfg[QR]);
@@ -708,7 +754,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
         const real x = cs.zcovptot * zdtgdp;
         const real zpreclr = cl_div((zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
         const real zbeta1 = cl_div(((cl_div_known(sqrt(cl_div(pap_k, cc.paph_sfc)), c.rvrfactor, c.rvrfactor_rcp)) * zpreclr), fmax(zcovpclr, zepsec));
-        const real zbeta = c.rg_rpecons * cl_pow<real>(zbeta1, R(0.5777));
+        const real zbeta = c.rg_rpecons * cl_pow<real>(c, zbeta1, R(0.5777));
         const real zdenom = R(1.0) + (zbeta * c.ptsphy) * zcorqsice;
         const real zdpr = ((cl_div(((zcovpclr * zbeta) * (zqsice - zqe)), zdenom)) * zdp) * c.zrg_r;
         const real zdpevap = zdpr * zdtgdp;
@@ -728,6 +774,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (zanew < c.ramin) zanew = R(0.0);
     const real zda = zanew - zaorig;
     cs.zanewm1 = zanew;
+    // the hook: the k-caching kernel issues the next level's first-consumed
+    // loads here (PF 3), after the physics' peak of live temporaries
+    mid();
 
     // 5.2 truncate explicit sinks, species in order (:2233-2286).
     // Column m of zsolqa (zsolqa[n][m], n=0..4) in C indexing; for each m the
@@ -935,7 +984,7 @@ CLOUDSC_HD ColConst<real> column_constants(const P& c, const KArgs<real>& A,
   const bool land = plsm > R(0.5);
   cc.kk_const = land ? sval(c.rcl_kk_cloud_num_land) : sval(c.rcl_kk_cloud_num_sea);
   cc.kk_lcrit = land ? sval(c.rclcrit_land) : sval(c.rclcrit_sea);
-  cc.kk_pow = cl_pow<real>(cc.kk_const, c.rcl_kkbaun);   // loop-invariant factor of the KK autoconversion (:1721)
+  cc.kk_pow = cl_pow<real>(c, cc.kk_const, c.rcl_kkbaun);   // loop-invariant factor of the KK autoconversion (:1721)
   return cc;
 }
 
@@ -973,8 +1022,8 @@ CLOUDSC_HD void init_carry(CS& cs) {
 // kcache_levels runs levels [lev0, lev1) of block b for one (active) lane with
 // the carried state `cs`; the plain kernel runs [0, klev) in one go, the
 // persistent kernel (below) runs a column in level segments.
-template <typename real, int PF, bool AER, typename CS>
-__device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar, int b,
+template <typename real, int PF, bool AER, typename PT, typename CS>
+__device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpar, int b,
                                               unsigned lo0, int lev0, int lev1, CS& cs) {
   if (lev0 >= lev1) return;
   const unsigned lo = lo0;                         // empty segment: no loads at lev0 (may be == klev)
@@ -982,7 +1031,7 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
   // registers, 2 = like 0, and the neighbour-level values (paph/pmfu/pmfd/plu of
   // k, k+1) re-read every level instead of carried (fewer live registers,
   // more L2 traffic)
-  constexpr bool PFX = PF == 1, NBR = PF == 2;
+  constexpr bool PFX = PF == 1, NBR = PF == 2, PFM = PF == 3;
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int nproma = A0.nproma, klev = A0.klev;
   const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
@@ -993,6 +1042,7 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
   ColConst<real> cc;
   Neighbors<real> nb;
   LevelIn<real> cur, nxt;
+  EarlyIn<real> nxt_e;
   int ncldtop0;
   {
     CLOUDSC_PARAMS_HERE;
@@ -1008,6 +1058,7 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
     nb.pmfd_n = ldg(A.pmfd, u2 + (size_t)l1 * nproma, lo);
     nb.plu_n = ldg(A.plu, u2 + (size_t)l1 * nproma, lo);
     if (PFX) load_level<real, AER>(cur, A, u2, u3, lev0, klev, nproma, lo);
+    if (PFM) load_early<real>(nxt_e, A, u2, u3, lev0, klev, nproma, lo);
   }
 
   for (int kloop = lev0; kloop < lev1; kloop++) {
@@ -1027,7 +1078,11 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
       const int k1 = k + 1 < klev ? k + 1 : klev - 1;
       const int k2 = k + 2 < klev ? k + 2 : klev - 1;
       const int kh2 = k + 2 < klev + 1 ? k + 2 : klev;
-      if (!PFX) load_level<real, AER>(cur, A, u2, u3, k, klev, nproma, lo);
+      if (!PFX && !PFM) load_level<real, AER>(cur, A, u2, u3, k, klev, nproma, lo);
+      if (PFM) {
+        load_late<real, AER>(cur, A, u2, k, nproma, lo);
+        take_early(cur, nxt_e);
+      }
       if (PFX) load_level<real, AER>(nxt, A, u2, u3, k1, klev, nproma, lo);
       if (NBR) {
         nb.paph_k = ldg(A.paph, uh + (size_t)k * nproma, lo);
@@ -1053,13 +1108,24 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<DevPara
       po.plude_k = cur.plude;
       po.atend = R(0.0);
       po.zcovptot_out = R(0.0);
+      // PF 3: the next level's early inputs, issued in the middle of this level
+      // (clamped at the last level: a re-read of valid data, never consumed)
+      const auto mid = [&]() {
+        if (PFM) {
+          const int k1 = k + 1 < klev ? k + 1 : klev - 1;
+          load_early<real>(nxt_e, *(const KArgs<real>*)launder_uniform(ka), u2, u3, k1, klev, nproma,
+                           launder_vgpr(lo0));
+        }
+      };
 #ifndef CLOUDSC_ABLATE_PHYSICS   // timing-only diagnostic build: the level loop without sections 3-6
-      if (physics) physics_level(c, k, klev, ncldtop0, cur, nb, cc, ls, cs, po);
+      if (physics) physics_level(c, k, klev, ncldtop0, cur, nb, cc, ls, cs, po, mid);
+      else mid();
 #else                            // (every load kept alive, so the bytes moved are the same)
       asm volatile("" :: "v"(cur.phrsw), "v"(cur.phrlw), "v"(cur.pvervel), "v"(cur.psnde), "v"(cur.psupsat),
                    "v"(nb.pmfu_k), "v"(nb.pmfd_k), "v"(nb.plu_n), "v"(cc.kk_pow));
       asm volatile("" :: "v"(cur.pclv[0]), "v"(cur.pclv[1]), "v"(cur.pclv[2]), "v"(cur.pclv[3]),
                    "v"(cur.ttcld[0]), "v"(cur.ttcld[1]), "v"(cur.ttcld[2]), "v"(cur.ttcld[3]));
+      mid();
 #endif
     }
     {
@@ -1088,8 +1154,8 @@ struct CarryRegs : CarryState<real> {
 template <typename real, bool LDSC>
 using CarryOf = typename std::conditional<LDSC, CarryLds<real>, CarryRegs<real>>::type;
 
-template <typename real, int PF, bool AER, bool LDSC>
-__device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar) {
+template <typename real, int PF, bool AER, bool LDSC, typename PT>
+__device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<PT> cpar) {
   const KArgs<real>& A = *(const KArgs<real>*)ka;
   const int b = blockIdx.x, jl = threadIdx.x;
   if (jl >= A.nproma || b * A.nproma + jl >= A.ngptot) return;
@@ -1167,8 +1233,8 @@ __device__ __forceinline__ void carry_io(real* st, size_t u, size_t plane, unsig
 #undef CLOUDSC_CARRY_IO
 }
 
-template <typename real, int PF, bool AER, bool LDSC>
-__device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar,
+template <typename real, int PF, bool AER, bool LDSC, typename PT>
+__device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>> ka, cptr<PT> cpar,
                                                                const PersistArgs<real>& P) {
   __shared__ int s_item;
   const KArgs<real>& A = *(const KArgs<real>*)ka;

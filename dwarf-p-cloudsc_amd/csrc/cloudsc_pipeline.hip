@@ -197,12 +197,12 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
   int rc = validate_run_args(p->device, p->precision, variant, p->ngptot, p->nproma, p->klev);
   if (rc) return rc;
   HIPCHK(hipSetDevice(p->device));
+  const int vk = variant_kind(variant);   // without the option bits
   const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
   // workspaces for the chunk size (SCC / KSEG), allocated on first use
   for (auto& s : p->slots) {
-    if (variant == CLOUDSC_VARIANT_KCACHE || variant == CLOUDSC_VARIANT_SCC_PRIVATE || s.scratch_variant == variant)
-      continue;
-    const long long nb = cloudsc_gpu_scratch_bytes(p->precision, variant, p->chunk_blocks * p->nproma, p->nproma,
+    if (vk == CLOUDSC_VARIANT_KCACHE || vk == CLOUDSC_VARIANT_SCC_PRIVATE || s.scratch_variant == vk) continue;
+    const long long nb = cloudsc_gpu_scratch_bytes(p->precision, vk, p->chunk_blocks * p->nproma, p->nproma,
                                                    p->klev);
     if (nb <= 0) return CLOUDSC_EINVAL;
     if ((size_t)nb > s.scratch_bytes) {
@@ -212,7 +212,7 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
       s.scratch = q;
       s.scratch_bytes = (size_t)nb;
     }
-    s.scratch_variant = variant;
+    s.scratch_variant = vk;
   }
   const void* const* hf = (const void* const*)&p->host;
   // all streams start after ev0 (recorded on the null stream) and ev1 waits for all of them
@@ -258,7 +258,7 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
   // KSEG: a timed-out segment hand-off in any chunk invalidates the step (the
   // error word of a slot's workspace accumulates over its chunks)
   // (every slot's word is read and cleared, also after the first failure)
-  if (variant == CLOUDSC_VARIANT_KSEG)
+  if (vk == CLOUDSC_VARIANT_KSEG)
     for (auto& s : p->slots) {
       const int r = kseg_check(p->device, s.st, s.scratch);
       if (r && !rc) rc = r;

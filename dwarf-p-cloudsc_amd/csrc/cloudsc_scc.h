@@ -144,8 +144,8 @@ struct PrivTemps {
   __device__ __forceinline__ real get_pfx(int m, int kh) const { return pfx[m][kh]; }
 };
 
-template <typename real, bool AER, typename Temps>
-__device__ __forceinline__ void cloudsc_scc_sweeps(cptr<KArgs<real>> ka, Temps& T, cptr<DevParams<real>> cpar) {
+template <typename real, bool AER, typename Temps, typename PT>
+__device__ __forceinline__ void cloudsc_scc_sweeps(cptr<KArgs<real>> ka, Temps& T, cptr<PT> cpar) {
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int nproma = A0.nproma, klev = A0.klev;
   const int b = blockIdx.x, jl = threadIdx.x;
@@ -156,7 +156,7 @@ __device__ __forceinline__ void cloudsc_scc_sweeps(cptr<KArgs<real>> ka, Temps& 
   const size_t u3 = (size_t)b * 5 * klev * nproma;
   const int ncldtop0 = ((const DevParams<real>*)cpar)->ncldtop - 1;
 #define SCC_A (*(const KArgs<real>*)launder_uniform(ka))
-#define SCC_C (*(const DevParams<real>*)launder_uniform(cpar))
+#define SCC_C (*(const PT*)launder_uniform(cpar))
 
   // ---- sweep 1: section 1 for every level ----
   for (int k = 0; k < klev; k++) {
@@ -234,9 +234,8 @@ __device__ __forceinline__ void cloudsc_scc_sweeps(cptr<KArgs<real>> ka, Temps& 
 }
 
 // config 2 / a4: the temporaries in the caller's HBM workspace
-template <typename real, bool AER>
-__device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const SccScratch<real> S,
-                                                 cptr<DevParams<real>> cpar) {
+template <typename real, bool AER, typename PT>
+__device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const SccScratch<real> S, cptr<PT> cpar) {
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int b = blockIdx.x, jl = threadIdx.x;
   if (jl >= A0.nproma || b * A0.nproma + jl >= A0.ngptot) return;
@@ -245,8 +244,8 @@ __device__ __forceinline__ void cloudsc_scc_body(cptr<KArgs<real>> ka, const Scc
 }
 
 // a3: the temporaries in per-thread private arrays (klev <= kPrivKlev, checked at launch)
-template <typename real, bool AER>
-__device__ __forceinline__ void cloudsc_scc_private_body(cptr<KArgs<real>> ka, cptr<DevParams<real>> cpar) {
+template <typename real, bool AER, typename PT>
+__device__ __forceinline__ void cloudsc_scc_private_body(cptr<KArgs<real>> ka, cptr<PT> cpar) {
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int b = blockIdx.x, jl = threadIdx.x;
   if (jl >= A0.nproma || b * A0.nproma + jl >= A0.ngptot) return;

@@ -268,10 +268,11 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
   if (!s || reps <= 0) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(s->device));
   void* scratch = nullptr;
-  if (variant == CLOUDSC_VARIANT_SCC || variant == CLOUDSC_VARIANT_KSEG) {   // workspaces, allocated on first use
-    void*& ws = variant == CLOUDSC_VARIANT_SCC ? s->scratch : s->kseg_ws;
+  const int vk = variant_kind(variant);   // without the option bits
+  if (vk == CLOUDSC_VARIANT_SCC || vk == CLOUDSC_VARIANT_KSEG) {   // workspaces, allocated on first use
+    void*& ws = vk == CLOUDSC_VARIANT_SCC ? s->scratch : s->kseg_ws;
     if (!ws) {
-      const long long nb = cloudsc_gpu_scratch_bytes(s->precision, variant, s->ngptot, s->nproma, s->klev);
+      const long long nb = cloudsc_gpu_scratch_bytes(s->precision, vk, s->ngptot, s->nproma, s->klev);
       if (nb <= 0) return CLOUDSC_EINVAL;
       int rc0 = dalloc(s, &ws, (size_t)nb);
       if (rc0) return rc0;
@@ -298,7 +299,7 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     if (ms) ms[r] = t;
   }
   for (auto& x : ev) (void)hipEventDestroy(x);
-  if (rc == CLOUDSC_OK && variant == CLOUDSC_VARIANT_KSEG) {
+  if (rc == CLOUDSC_OK && vk == CLOUDSC_VARIANT_KSEG) {
     // a segment whose predecessor never arrived gives up after a bounded spin
     // and counts itself in the workspace's error word: its results are
     // invalid.  The count accumulates over the reps of this call (the word is

@@ -54,7 +54,7 @@
 
 typedef struct {
   int numomp, ngptot, nproma, ngpus, precision, variant, reps, warmup;
-  int transfer, chunk_blocks, nstreams;
+  int transfer, chunk_blocks, nstreams, exact_libm;
   double tol;
   int tol_given;
   const char *input_h5, *reference_h5, *data_dir, *write_h5_dir;
@@ -62,6 +62,7 @@ typedef struct {
 
 typedef struct {
   int device, ngptot, nproma, precision, variant, reps, warmup;
+  int libm_bit;                   /* CLOUDSC_FP32_EXACT_LIBM or 0 */
   long long col_offset;
   const cloudsc_template_t *tmpl;
   const cloudsc_params_t *params;
@@ -98,6 +99,8 @@ static void usage(const char *prog) {
           "  --precision fp64|fp32 (default fp64)\n"
           "  --variant kseg|kcache|scc|scc-private|cpu (default kseg; cpu = the library's CPU variant on\n"
           "                        <nthreads> host threads, host-memory fields: BASELINE config 1)\n"
+          "  --fp32-exact-libm     fp32: exp/pow with the glibc algorithms (bit-identical to the fp32\n"
+          "                        restatement) instead of the default float-internal device forms\n"
           "  --reps R              timed steps (default 1)\n"
           "  --warmup W            untimed steps before the timed ones (default 1)\n"
           "  --input FILE          input HDF5 file (default ./input.h5 when present)\n"
@@ -148,6 +151,7 @@ static int parse(int argc, char **argv, options_t *o) {
     else if (!strcmp(a, "--tol")) { NEEDV(); o->tol = atof(v); o->tol_given = 1; }
     else if (!strcmp(a, "--write-h5")) { NEEDV(); o->write_h5_dir = v; }
     else if (!strcmp(a, "--transfer")) o->transfer = 1;
+    else if (!strcmp(a, "--fp32-exact-libm")) o->exact_libm = 1;
     else if (!strcmp(a, "--chunk")) { NEEDV(); o->chunk_blocks = atoi(v); }
     else if (!strcmp(a, "--streams")) { NEEDV(); o->nstreams = atoi(v); }
     else if (!strcmp(a, "-h") || !strcmp(a, "--help")) return -1;
@@ -202,14 +206,14 @@ static void *shard_main(void *arg) {
                                s->params);
   if (!s->rc && s->warmup > 0) {
     float *w = (float *)malloc(sizeof(float) * s->warmup);
-    s->rc = w ? cloudsc_state_run(st, s->variant, s->warmup, w) : CLOUDSC_ENOMEM;
+    s->rc = w ? cloudsc_state_run(st, s->variant | s->libm_bit, s->warmup, w) : CLOUDSC_ENOMEM;
     free(w);
   }
   if (!s->rc) s->rc = cloudsc_state_sync(st);
   /* every shard reaches the barrier, also after an error, so nobody waits forever */
   pthread_barrier_wait(s->barrier);
   s->t_start = now();
-  if (!s->rc) s->rc = cloudsc_state_run(st, s->variant, s->reps, s->kernel_ms);
+  if (!s->rc) s->rc = cloudsc_state_run(st, s->variant | s->libm_bit, s->reps, s->kernel_ms);
   if (!s->rc) s->rc = cloudsc_state_sync(st);
   s->t_end = now();
   pthread_barrier_wait(s->barrier);
@@ -312,7 +316,7 @@ static int run_host(const options_t *o, const cloudsc_dataset_t *ds) {
       if (r >= o->warmup)
         for (int t = 0; t < nth; t++) { th_s[t] += th_step[t]; th_blk[t] += th_blk_step[t]; th_col[t] += th_col_step[t]; }
     } else {
-      rc = cloudsc_host_pipeline_run(pipe, o->variant, &ms);
+      rc = cloudsc_host_pipeline_run(pipe, o->variant | (o->exact_libm ? CLOUDSC_FP32_EXACT_LIBM : 0), &ms);
     }
     if (r >= o->warmup) total_ms += ms;
   }
@@ -452,7 +456,7 @@ int main(int argc, char **argv) {
   cloudsc_io_reference(&ds, &ref);
   const int nblocks = o.ngptot / o.nproma + (o.ngptot % o.nproma ? 1 : 0);
   printf(" CLOUDSC-AMD: %s, variant %s, %d device(s); state: %s (KLON=%d, KLEV=%d)\n",
-         o.precision == CLOUDSC_FP64 ? "fp64" : "fp32",
+         o.precision == CLOUDSC_FP64 ? "fp64" : (o.exact_libm ? "fp32 (glibc expf/powf)" : "fp32"),
          variant_name(o.variant),
          o.ngpus, ds.source, ds.klon, ds.klev);
 
@@ -472,6 +476,7 @@ int main(int argc, char **argv) {
     shard_t *s = &sh[nused++];
     s->device = d % ndev; s->ngptot = (int)cols; s->col_offset = col; s->nproma = o.nproma;
     s->precision = o.precision; s->variant = o.variant; s->reps = o.reps; s->warmup = o.warmup;
+    s->libm_bit = o.exact_libm ? CLOUDSC_FP32_EXACT_LIBM : 0;
     s->tmpl = &tmpl; s->params = &ds.params; s->ref = ds.has_reference ? &ref : NULL; s->barrier = &bar;
     s->kernel_ms = (float *)calloc((size_t)o.reps, sizeof(float));
     col += cols;

@@ -72,6 +72,15 @@ extern "C" {
                                    /* the reference CUDA SCC form, cloudsc_c.cu:60-317; klev <= 137 as    */
                                    /* there (:53); no caller workspace                                     */
 
+/* Option bit, OR-ed into a `variant` argument (cloudsc_gpu_run, cloudsc_state_run,
+ * cloudsc_host_pipeline_run).  fp32 evaluates exp/pow in single precision with
+ * the device's float forms by default (hardware exp2/log2 with an exact
+ * argument reduction: <= 2 ulp, every operation float); with this bit it uses
+ * the reference CPU build's glibc expf/powf algorithms instead (computed in
+ * double, bit-identical to the single-precision restatement, slower).  fp64
+ * always uses the reference CPU build's exp/pow and ignores the bit. */
+#define CLOUDSC_FP32_EXACT_LIBM 0x100
+
 /* error codes */
 #define CLOUDSC_OK            0
 #define CLOUDSC_EINVAL      (-1)   /* bad argument (sizes, NULL pointer, precision, variant) */
@@ -192,6 +201,12 @@ int cloudsc_debug_set_kseg_spin_limit(long long limit);
  * The result bits do not depend on either; the tests use it to exercise the
  * hand-offs with few workgroups and many segments. */
 int cloudsc_debug_set_kseg_schedule(int nseg, int grid);
+
+/* Diagnostic: the kernels' single-precision exp/pow on the device, element-wise
+ * over n host values: which = 0 the float-internal expf (CLOUDSC_FP32 default),
+ * 1 its powf(x, y), 2 the glibc-algorithm expf (CLOUDSC_FP32_EXACT_LIBM),
+ * 3 its powf.  y is read for 1 and 3 only. */
+int cloudsc_debug_fp32_libm(int device, int which, const float *x, const float *y, float *out, long long n);
 
 /* Human-readable message for an error code; last HIP error string of this thread. */
 const char *cloudsc_strerror(int code);

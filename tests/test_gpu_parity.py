@@ -580,13 +580,17 @@ def test_dwarf_tolerance_vs_reference_h5(lib, ds):
         assert rel <= 10 * eps, (name, rel)
 
 
-# fp32: the device expf/powf are the host C library's single-precision
-# algorithms too (csrc/cloudsc_libm.h), so the fp32 kernels reproduce the fp32
-# restatement (JPRB=sp semantics: float storage and constants, expf/powf) bit
-# for bit.
+# fp32 with CLOUDSC_FP32_EXACT_LIBM: the device expf/powf are the host C
+# library's single-precision algorithms too (csrc/cloudsc_libm.h), so the fp32
+# kernels reproduce the fp32 restatement (JPRB=sp semantics: float storage and
+# constants, expf/powf) bit for bit.  (The default fp32 forms are float-internal:
+# tolerance tests below.)
+EXACT = ca.FP32_EXACT_LIBM
+
+
 @pytest.mark.parametrize("variant", [ca.VARIANT_KCACHE, ca.VARIANT_KSEG, ca.VARIANT_SCC])
 def test_bitwise_fp32_vs_oracle(lib, ds, oracle_mod, variant):
-    out = run_gpu(ds, 1000, 128, precision=ca.FP32, variant=variant)
+    out = run_gpu(ds, 1000, 128, precision=ca.FP32, variant=variant | EXACT)
     ref = oracle_outputs(oracle_mod, ds, 1000, 128, precision=ca.FP32)
     bad = {}
     for _, k in ca.VALIDATED:
@@ -602,7 +606,7 @@ def test_bitwise_fp32_vs_oracle(lib, ds, oracle_mod, variant):
 def test_bitwise_fp32_scenarios(lib, ds, scenarios, oracle_mod, case):
     import make_fixtures as mf
     s = mf.perturbed(ds, 1) if case == "seed1" else scenarios[case]
-    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=ca.VARIANT_KCACHE)
+    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=ca.VARIANT_KCACHE | EXACT)
     ref = oracle_outputs(oracle_mod, s, 300, 64, precision=ca.FP32)
     for _, k in ca.VALIDATED:
         a = np.ascontiguousarray(out[k], dtype=np.float32).view(np.uint32)
@@ -638,9 +642,96 @@ def test_bitwise_fp32_other_configurations(lib, ds, oracle_mod, case, variant):
     else:
         s = ds.copy()
         s.params["nssopt"] = 3
-    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=variant)
+    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=variant | EXACT)
     ref = oracle_outputs(oracle_mod, s, 300, 64, precision=ca.FP32)
     for _, k in ca.VALIDATED:
         a = np.ascontiguousarray(out[k], dtype=np.float32).view(np.uint32)
         r = np.ascontiguousarray(ref[k], dtype=np.float32).view(np.uint32)
         assert np.array_equal(a, r), (k, int(np.count_nonzero(a != r)))
+
+
+# ---- fp32 default: float-internal exp/pow (SURVEY.md §8c tolerance gates) ----
+RELL1_FP32_FAST = 1e-4     # per field, vs the fp32 restatement (glibc expf/powf)
+
+
+def fp32_gates(out, ref, gold, cpu_vs_gold):
+    """relL1 <= 1e-4 per field vs the fp32 restatement, and vs reference.h5 no
+    worse than 2x the fp32 restatement's own error plus a floor."""
+    rep = field_report(out, ref)
+    for k, v in sorted(rep.items(), key=lambda kv: -kv[1][0])[:6]:
+        print("fp32 fast libm vs fp32 restatement %-18s relL1 %.3e" % (k, v[0]))
+    bad = {k: v[0] for k, v in rep.items() if not v[0] <= RELL1_FP32_FAST}
+    assert bad == {}, bad
+    g = field_report(out, gold)
+    for k in g:
+        assert g[k][0] <= 2.0 * cpu_vs_gold[k][0] + 1e-6, (k, g[k][0], cpu_vs_gold[k][0])
+
+
+@pytest.mark.parametrize("variant", [ca.VARIANT_KSEG, ca.VARIANT_KCACHE, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE])
+def test_fp32_fast_libm_tolerance(lib, ds, oracle_mod, variant):
+    n = 1000
+    out = run_gpu(ds, n, 128, precision=ca.FP32, variant=variant)
+    ref = oracle_outputs(oracle_mod, ds, n, 128, precision=ca.FP32)
+    gold = {k: np.take(ds.reference[k], np.arange(n) % ds.klon, axis=-1) for _, k in ca.VALIDATED}
+    fp32_gates(out, ref, gold, field_report(ref, gold))
+
+
+@pytest.mark.parametrize("case", ["W", "M", "seed1", "aerosol", "nssopt3"])
+def test_fp32_fast_libm_tolerance_scenarios(lib, ds, scenarios, oracle_mod, case):
+    import make_fixtures as mf
+    if case in ("W", "M"):
+        s = scenarios[case]
+    elif case == "seed1":
+        s = mf.perturbed(ds, 1)
+    elif case == "aerosol":
+        s = mf.with_aerosols(ds)
+    else:
+        s = ds.copy()
+        s.params["nssopt"] = 3
+    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=ca.VARIANT_KSEG)
+    ref = oracle_outputs(oracle_mod, s, 300, 64, precision=ca.FP32)
+    rep = field_report(out, ref)
+    bad = {k: v[0] for k, v in rep.items() if not v[0] <= RELL1_FP32_FAST}
+    assert bad == {}, bad
+
+
+def test_fp32_exact_libm_bit_is_ignored_in_fp64(lib, ds):
+    a = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KSEG)
+    b = run_gpu(ds, 1000, 128, variant=ca.VARIANT_KSEG | EXACT)
+    assert bitwise_mismatches(a, b) == {}
+
+
+def ulp_distance(a, b):
+    """|a - b| in units in the last place of float32 (sign-magnitude ordering)."""
+    ia = np.ascontiguousarray(a, dtype=np.float32).view(np.int32).astype(np.int64)
+    ib = np.ascontiguousarray(b, dtype=np.float32).view(np.int32).astype(np.int64)
+    ia = np.where(ia < 0, -(ia & 0x7fffffff), ia)
+    ib = np.where(ib < 0, -(ib & 0x7fffffff), ib)
+    return np.abs(ia - ib)
+
+
+def test_fp32_fast_libm_ulp(lib):
+    """The float-internal expf / powf against the glibc-algorithm forms (which
+    are within 1 ulp of the exact values, tools/libm_check.cc) on the device,
+    over the argument ranges CLOUDSC uses (saturation exponents -40..20, the
+    snow / ice exponentials, pow bases 1e-12..1e8 with the parameter exponents
+    0.333 .. 1.5 and random ones): at most 2 ulp apart, most of them equal."""
+    import ctypes as C
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    x = np.concatenate([rng.uniform(-40.0, 20.0, n // 2), rng.uniform(-87.0, 87.0, n // 2)]).astype(np.float32)
+    px = (10.0 ** rng.uniform(-12.0, 8.0, n)).astype(np.float32)
+    py = np.concatenate([rng.choice(np.array([0.333, 0.4, 0.5777, 0.666, 1.5, 3.0, 2.47, -1.79], np.float32),
+                                    n // 2), rng.uniform(-3.0, 3.0, n // 2)]).astype(np.float32)
+    res = {}
+    for which in range(4):
+        out = np.empty(n, np.float32)
+        xs = x if which % 2 == 0 else px
+        ca.check(lib.cloudsc_debug_fp32_libm(0, which, xs.ctypes.data, py.ctypes.data, out.ctypes.data, n))
+        res[which] = out
+    d_exp = ulp_distance(res[0], res[2])
+    finite = np.isfinite(res[3]) & (res[3] > 1e-37) & (res[3] < 1e37)
+    d_pow = ulp_distance(res[1][finite], res[3][finite])
+    print("expf fast vs glibc: max %d ulp, %.1f %% equal; powf: max %d ulp, %.1f %% equal" % (
+        d_exp.max(), 100.0 * np.mean(d_exp == 0), d_pow.max(), 100.0 * np.mean(d_pow == 0)))
+    assert d_exp.max() <= 2 and d_pow.max() <= 2
