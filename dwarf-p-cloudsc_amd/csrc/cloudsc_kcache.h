@@ -1031,7 +1031,10 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
   // registers, 2 = like 0, and the neighbour-level values (paph/pmfu/pmfd/plu of
   // k, k+1) re-read every level instead of carried (fewer live registers,
   // more L2 traffic)
-  constexpr bool PFX = PF == 1, NBR = PF == 2, PFM = PF == 3;
+  // 3 = the first-consumed inputs of level k+1 (EarlyIn) issued in the middle
+  // of level k (the physics' mid hook), the rest at the top of level k+1;
+  // 4 = all inputs of level k+1 issued in the middle of level k
+  constexpr bool PFX = PF == 1, NBR = PF == 2, PFM = PF == 3, PFA = PF == 4;
   const KArgs<real>& A0 = *(const KArgs<real>*)ka;
   const int nproma = A0.nproma, klev = A0.klev;
   const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
@@ -1059,6 +1062,7 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
     nb.plu_n = ldg(A.plu, u2 + (size_t)l1 * nproma, lo);
     if (PFX) load_level<real, AER>(cur, A, u2, u3, lev0, klev, nproma, lo);
     if (PFM) load_early<real>(nxt_e, A, u2, u3, lev0, klev, nproma, lo);
+    if (PFA) load_level<real, AER>(nxt, A, u2, u3, lev0, klev, nproma, lo);
   }
 
   for (int kloop = lev0; kloop < lev1; kloop++) {
@@ -1078,7 +1082,8 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
       const int k1 = k + 1 < klev ? k + 1 : klev - 1;
       const int k2 = k + 2 < klev ? k + 2 : klev - 1;
       const int kh2 = k + 2 < klev + 1 ? k + 2 : klev;
-      if (!PFX && !PFM) load_level<real, AER>(cur, A, u2, u3, k, klev, nproma, lo);
+      if (!PFX && !PFM && !PFA) load_level<real, AER>(cur, A, u2, u3, k, klev, nproma, lo);
+      if (PFA) cur = nxt;
       if (PFM) {
         load_late<real, AER>(cur, A, u2, k, nproma, lo);
         take_early(cur, nxt_e);
@@ -1111,10 +1116,14 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
       // PF 3: the next level's early inputs, issued in the middle of this level
       // (clamped at the last level: a re-read of valid data, never consumed)
       const auto mid = [&]() {
-        if (PFM) {
+        if (PFM || PFA) {
           const int k1 = k + 1 < klev ? k + 1 : klev - 1;
-          load_early<real>(nxt_e, *(const KArgs<real>*)launder_uniform(ka), u2, u3, k1, klev, nproma,
-                           launder_vgpr(lo0));
+          if (PFM)
+            load_early<real>(nxt_e, *(const KArgs<real>*)launder_uniform(ka), u2, u3, k1, klev, nproma,
+                             launder_vgpr(lo0));
+          else
+            load_level<real, AER>(nxt, *(const KArgs<real>*)launder_uniform(ka), u2, u3, k1, klev, nproma,
+                                  launder_vgpr(lo0));
         }
       };
 #ifndef CLOUDSC_ABLATE_PHYSICS   // timing-only diagnostic build: the level loop without sections 3-6

@@ -28,11 +28,31 @@
 #include <stddef.h>
 #include <omp.h>
 
+/* Sensitivity probe (fp32 only, off by default): with a non-zero seed every
+ * expf/powf result is moved by -1, 0 or +1 ulp, chosen by a hash of its
+ * arguments and the seed -- a libm that is faithful but not glibc's.  The
+ * outputs' response to it is the noise floor against which a different
+ * single-precision exp/pow (the GPU's float-internal forms) is gated
+ * (tests/test_gpu_parity.py, SURVEY.md §8c "±1-ulp emulation"). */
+extern unsigned cloudsc_oracle_libm_nudge_seed;
+
 #ifdef ORACLE_SP
 typedef float real;
+static inline float nudge_f(float r, unsigned a, unsigned b)
+{
+  const unsigned seed = cloudsc_oracle_libm_nudge_seed;
+  if (!seed || !(r == r) || r == 0.0f || fabsf(r) > FLT_MAX) return r;
+  unsigned h = (a * 2654435761u) ^ (b * 2246822519u) ^ (seed * 3266489917u);
+  h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+  const int d = (int)(h % 3u) - 1;
+  return d == 0 ? r : nextafterf(r, d > 0 ? INFINITY : -INFINITY);
+}
+static inline unsigned fbits(float x) { union { float f; unsigned u; } v = {x}; return v.u; }
+static inline float expf_probe(float x) { return nudge_f(expf(x), fbits(x), 0x9e3779b9u); }
+static inline float powf_probe(float x, float y) { return nudge_f(powf(x, y), fbits(x), fbits(y)); }
 #define L(x) x##f
-#define EXP expf
-#define POW powf
+#define EXP expf_probe
+#define POW powf_probe
 #define SQRT sqrtf
 #define FMIN fminf
 #define FMAX fmaxf
@@ -909,6 +929,9 @@ int BLOCK_FN(const cloudsc_params_t *p, int kidia, int kfdia, int klon, int klev
 }
 
 #ifndef ORACLE_SP
+unsigned cloudsc_oracle_libm_nudge_seed = 0;
+void cloudsc_oracle_set_libm_nudge(unsigned seed) { cloudsc_oracle_libm_nudge_seed = seed; }
+
 /* The driver entry is compiled once (in the fp64 object). */
 int cloudsc_oracle_run(int nthreads, int precision, int ngptot, int nproma, int klev,
                        const cloudsc_params_t *p, const cloudsc_fields_t *f, double *seconds)

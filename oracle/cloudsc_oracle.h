@@ -34,6 +34,12 @@ int cloudsc_oracle_block_sp(const cloudsc_params_t *p, int kidia, int kfdia, int
 int cloudsc_oracle_run(int nthreads, int precision, int ngptot, int nproma, int klev,
                        const cloudsc_params_t *p, const cloudsc_fields_t *f, double *seconds);
 
+/* Sensitivity probe of the fp32 restatement: seed != 0 moves every expf/powf
+ * result by -1, 0 or +1 ulp (a hash of the arguments and the seed picks which);
+ * 0 restores the plain C library results.  Not thread-safe against a running
+ * cloudsc_oracle_run. */
+void cloudsc_oracle_set_libm_nudge(unsigned seed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -56,14 +56,21 @@ def ref_lib():
 
 
 def run_oracle(ds: "ca.Dataset", ngptot: int, nproma: int, precision: int = ca.FP64,
-               nthreads: int = 0, col_offset: int = 0):
-    """Expand ds to ngptot columns, run the restatement. Returns (HostState, seconds)."""
+               nthreads: int = 0, col_offset: int = 0, libm_nudge: int = 0):
+    """Expand ds to ngptot columns, run the restatement. Returns (HostState, seconds).
+    libm_nudge (fp32 only): a non-zero seed moves every expf/powf result by -1/0/+1 ulp
+    (cloudsc_oracle_set_libm_nudge) -- the sensitivity probe of the fp32 gates."""
     st = ca.make_host_state(ds, ngptot, nproma, precision, col_offset)
     p = ca.Params.from_dict(ds.params)
     f = st.fields()
     secs = C.c_double()
-    rc = oracle_lib().cloudsc_oracle_run(nthreads, precision, ngptot, nproma, ds.klev,
-                                         C.byref(p), C.byref(f), C.byref(secs))
+    lib = oracle_lib()
+    lib.cloudsc_oracle_set_libm_nudge(C.c_uint(libm_nudge))
+    try:
+        rc = lib.cloudsc_oracle_run(nthreads, precision, ngptot, nproma, ds.klev,
+                                    C.byref(p), C.byref(f), C.byref(secs))
+    finally:
+        lib.cloudsc_oracle_set_libm_nudge(C.c_uint(0))
     if rc != 0:
         raise RuntimeError("cloudsc_oracle_run failed: %d" % rc)
     return st, secs.value
