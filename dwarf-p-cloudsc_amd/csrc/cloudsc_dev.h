@@ -67,15 +67,31 @@ struct DevParams {
 // algorithms).  The phase functions take the block as `const P& c` and pass it
 // to cl_exp / cl_pow, so the choice costs nothing at run time.  fp64 is always
 // the reference's algorithms (FAST is only instantiated for float).
-template <typename real, bool FAST>
+// VREG: the block copied into VGPRs for the level loop (fp32 k-caching kernels,
+// kcache_levels) instead of being read with a scalar load at each use.
+template <typename real, bool FAST, bool VREG = false>
 struct DevParamsT : DevParams<real> {};
 template <typename P>
 struct LibmFast {
   static constexpr bool value = false;
 };
-template <>
-struct LibmFast<DevParamsT<float, true>> {
+template <bool VREG>
+struct LibmFast<DevParamsT<float, true, VREG>> {
   static constexpr bool value = true;
+};
+template <typename P>
+struct ParamsInVgprs {
+  static constexpr bool value = false;
+};
+template <typename real, bool FAST>
+struct ParamsInVgprs<DevParamsT<real, FAST, true>> {
+  static constexpr bool value = true;
+};
+template <typename P>
+struct WithVgprParams;
+template <typename real, bool FAST, bool VREG>
+struct WithVgprParams<DevParamsT<real, FAST, VREG>> {
+  using type = DevParamsT<real, FAST, true>;
 };
 
 // The phase functions of the physics (cloudsc_kcache.h) and the helpers below
@@ -113,6 +129,13 @@ CLOUDSC_HD T sval(T v) {
   asm volatile("" : "+s"(v));
 #endif
   return v;
+}
+// sval for a parameter of the block `c`: a no-op when the block already lives
+// in VGPRs (an SGPR constraint on a VGPR value would be an illegal copy)
+template <typename P, typename T>
+CLOUDSC_HD T pval(const P&, T v) {
+  if constexpr (ParamsInVgprs<P>::value) return v;
+  else return sval(v);
 }
 template <typename T>
 CLOUDSC_HD T launder_vgpr(T v) {

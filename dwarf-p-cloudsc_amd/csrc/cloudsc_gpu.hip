@@ -215,9 +215,11 @@ namespace {
 // Kernel configuration: occupancy target (waves per SIMD, via __launch_bounds__)
 // x load schedule (PF) x where the carried state lives (LDSC).  The product
 // library instantiates only the measured defaults:
-//   fp64: 2 waves/SIMD, carried state and neighbour planes in registers (cfg 20)
-//         -- with the streaming I/O 1.8 % faster than the LDS-carry cfg 122
-//         (profiles/r01/sweep_kseg_cfgs_nt.jsonl);
+//   fp64: 2 waves/SIMD, carried state and neighbour planes in registers, the
+//         next level's first-consumed inputs issued in the middle of the level
+//         (cfg 23, PF 3; round 3: 0.8 % faster than cfg 20 on two boxes,
+//         profiles/r03/sweep_pf3_fp64.jsonl; cfg 20 was 1.8 % faster than the
+//         LDS-carry cfg 122, profiles/r01/sweep_kseg_cfgs_nt.jsonl);
 //   fp32: 2 waves/SIMD with the register prefetch of level k+1 (cfg 21) -- 1.8-3.5 %
 //         faster than round 1's 3-wave cfg 31 on the same box (profiles/r02/fp32_cfg_sweep.jsonl;
 //         cfg 31 was 2-3 % faster than the 4-wave LDS-carry cfg 140, sweep_fp32_cfgs_libm.jsonl).
@@ -225,7 +227,7 @@ namespace {
 // whole table and reads CLOUDSC_KCACHE_CFG / CLOUDSC_KSEG_* from the environment
 // (tools/sweep.py); the product library never reads the environment.
 template <typename real> struct DefaultCfg;
-template <> struct DefaultCfg<double> { static constexpr int code = 20, waves = 2, pf = 0; };
+template <> struct DefaultCfg<double> { static constexpr int code = 23, waves = 2, pf = 3; };
 template <> struct DefaultCfg<float> { static constexpr int code = 21, waves = 2, pf = 1; };
 
 #ifdef CLOUDSC_DEBUG_KNOBS

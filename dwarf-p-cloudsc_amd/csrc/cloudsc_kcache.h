@@ -467,7 +467,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
 
     // 3.4 erosion of clouds by turbulent mixing (:1087-1118)
-    const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? sval(c.zldifdt_conv) : sval(c.zldifdt0);
+    const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? pval(c, c.zldifdt_conv) : pval(c, c.zldifdt0);
     if (zli > zepsec) {
       const real ze = zldifdt * fmax(zqsmix - zqx[QV], R(0.0));
       real zleros = za * ze;
@@ -604,7 +604,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       fsrc_r = cs.pfx_r * zdtgdp; sa_rr = sa_rr + fsrc_r; zqxfg[QR] = zqxfg[QR] + fsrc_r; zqpretot = zqpretot + zqxfg[QR];
       fsrc_s = cs.pfx_s * zdtgdp; sa_ss = sa_ss + fsrc_s; zqxfg[QS] = zqxfg[QS] + fsrc_s; zqpretot = zqpretot + zqxfg[QS];
     }
-    const real vqx_i = c.laericesed ? R(0.002) * in.pre_ice : sval(c.rvice);
+    const real vqx_i = c.laericesed ? R(0.002) * in.pre_ice : pval(c, c.rvice);
     const real fsink_i = zdtgdp * (vqx_i * zrho);
     const real fsink_r = zdtgdp * (c.rvrain * zrho);
     const real fsink_s = zdtgdp * (c.rvsnow * zrho);
@@ -626,7 +626,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // 4.3a autoconversion to snow (:1616-1637)
     if (cold && zicecld > zepsec) {
       real zzco = c.zzco_snow * cl_exp<real>(c, c.rsnowlin2 * (ztp1 - c.rtt));
-      real zlcrit = sval(c.rlcritsnow);
+      real zlcrit = pval(c, c.rlcritsnow);
       if (c.laericeauto) {
         zlcrit = in.picrit_aer;
         zzco = zzco * cl_pow<real>(c, cl_div(c.rnice, in.pnice), R(0.333));
@@ -982,8 +982,8 @@ CLOUDSC_HD ColConst<real> column_constants(const P& c, const KArgs<real>& A,
   cc.ktype = ldg(A.ktype, u1, lo * (unsigned)(sizeof(int)) / (unsigned)sizeof(real));
   cc.paph_sfc = ldg(A.paph, uh + (size_t)A.klev * A.nproma, lo);
   const bool land = plsm > R(0.5);
-  cc.kk_const = land ? sval(c.rcl_kk_cloud_num_land) : sval(c.rcl_kk_cloud_num_sea);
-  cc.kk_lcrit = land ? sval(c.rclcrit_land) : sval(c.rclcrit_sea);
+  cc.kk_const = land ? pval(c, c.rcl_kk_cloud_num_land) : pval(c, c.rcl_kk_cloud_num_sea);
+  cc.kk_lcrit = land ? pval(c, c.rclcrit_land) : pval(c, c.rclcrit_sea);
   cc.kk_pow = cl_pow<real>(c, cc.kk_const, c.rcl_kkbaun);   // loop-invariant factor of the KK autoconversion (:1721)
   return cc;
 }
@@ -1010,6 +1010,14 @@ CLOUDSC_HD void init_carry(CS& cs) {
   cs.qxnm1_l = cs.qxnm1_i = R(0.0);
   cs.pfx_i = cs.pfx_r = cs.pfx_s = R(0.0);
   cs.fl_lf = cs.fl_if = cs.fl_lng = cs.fl_nng = cs.fl_ltur = cs.fl_itur = R(0.0);
+}
+
+// The level loop's parameter block: the VGPR copy (fp32) or the constant-space
+// block read with scalar loads (laundered: loads issued where used).
+template <bool PVR, typename PV, typename PT>
+__device__ __forceinline__ const auto& params_here(const PV& pv, cptr<PT> cpar) {
+  if constexpr (PVR) return pv;
+  else return *(const PT*)launder_uniform(cpar);
 }
 
 // ===================== SCC-k-caching kernel body =====================
@@ -1065,6 +1073,21 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
     if (PFA) load_level<real, AER>(nxt, A, u2, u3, lev0, klev, nproma, lo);
   }
 
+  // fp32: the parameter block copied into VGPRs once per call (each value an
+  // opaque per-lane copy), so the level loop reads every parameter from a
+  // register instead of a scalar load + lgkmcnt(0) wait at each use -- 5 %
+  // (profiles/r03/experiment_fp32_params_in_vgprs_ab.txt).  fp32 has the
+  // registers for it (~95 VGPRs on top of ~155 at 2 waves/SIMD); fp64 would
+  // need twice as many and keeps the scalar loads.
+  constexpr bool PVR = sizeof(real) == 4;
+  using PV = typename std::conditional<PVR, typename WithVgprParams<PT>::type, PT>::type;
+  PV pv;
+  if constexpr (PVR) {
+    pv = *(const PV*)(const PT*)cpar;
+    float* q = (float*)&pv;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(PV) / sizeof(float)) - 4; i++) asm volatile("" : "+v"(q[i]));   // not the 4 ints
+  }
   for (int kloop = lev0; kloop < lev1; kloop++) {
     // the level index is laundered too, so no per-field induction pointers are formed
     int k = kloop;
@@ -1106,7 +1129,7 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
     LevelState<real> ls;
     PhysOut<real> po;
     {
-      CLOUDSC_PARAMS_HERE;
+      const auto& c = params_here<PVR>(pv, cpar);
       init_level(c, cur, ls);
 #pragma unroll
       for (int m = 0; m < 4; m++) { po.zqxn[m] = R(0.0); po.ctend[m] = R(0.0); }
@@ -1139,7 +1162,7 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
     }
     {
       const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
-      CLOUDSC_PARAMS_HERE;
+      const auto& c = params_here<PVR>(pv, cpar);
       store_level(A, u2, u3, k, klev, nproma, lo, physics, ls, po);
       flux_level(c, A, uh + (size_t)(k + 1) * nproma, lo, cur, ls, po, nb.paph_k, nb.paph_n, cs);
     }
