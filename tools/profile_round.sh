@@ -27,6 +27,6 @@ d.update(json.load(open(src)))
 json.dump(d, open(dst, "w"), indent=1, sort_keys=True)
 PY
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/stats_${variant}_${prec} -o bench --output-format csv \
-  -- python3 $R/bench.py --steps 100 --warmup 5 --variant $variant --precision $prec --nproma $nproma \
+  -- python3 $R/bench.py --steps 100 --warmup 5 --no-transfer --variant $variant --precision $prec --nproma $nproma \
   > $out/bench_under_rocprof_${variant}_${prec}.log 2>&1 || exit $?
 cp $R/profiles/traffic_latest.json $out/traffic_latest.json
