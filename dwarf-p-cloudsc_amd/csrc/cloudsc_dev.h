@@ -481,6 +481,53 @@ CLOUDSC_HD real cl_div(typename std::common_type<real>::type n, typename std::co
   return cl_div(static_cast<real>(n), static_cast<real>(d));
 }
 
+// The physics' divisions: cl_div_p<real>(c, n, d), the form chosen by the
+// parameter block's type like cl_exp / cl_pow.  fp32 FAST kernels (the
+// CLOUDSC_FP32 default, tolerance-gated like the float-internal expf/powf):
+// v_rcp_f32 (1 ulp) and ONE residual correction,
+//   q0 = n*r,  q = fma(fma(-d, q0, n), r, q0)
+// -- the reciprocal + 3 operations instead of + 7 (cl_div's Newton-refined
+// reciprocal and two corrections, which make every quotient the IEEE one).
+// The correction leaves q within 1 ulp of n/d (almost always the IEEE
+// quotient).  fp64 and the exact fp32 forms (CLOUDSC_FP32_EXACT_LIBM) are cl_div.
+template <typename real, typename P>
+CLOUDSC_HD real cl_div_p(const P&, typename std::common_type<real>::type n, typename std::common_type<real>::type d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) {
+    const float r = __builtin_amdgcn_rcpf(d), q = n * r;
+    return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+  }
+#endif
+  return cl_div(static_cast<real>(n), static_cast<real>(d));
+}
+template <typename real, typename P>
+CLOUDSC_HD Recip<real> cl_recip_p(const P&, typename std::common_type<real>::type d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) return {d, __builtin_amdgcn_rcpf(d)};
+#endif
+  return cl_recip(static_cast<real>(d));
+}
+template <typename real, typename P>
+CLOUDSC_HD real cl_div_p(const P&, typename std::common_type<real>::type n, const Recip<real>& rd) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) {
+    const float q = n * rd.r;
+    return __builtin_fmaf(__builtin_fmaf(-rd.d, q, n), rd.r, q);
+  }
+#endif
+  return cl_div(static_cast<real>(n), rd);
+}
+// a known divisor with its RN(1/d): the FAST form is the same single
+// correction, the exact one cl_div's two (the IEEE quotient)
+template <typename real, typename P>
+CLOUDSC_HD real cl_div_known_p(const P& c, typename std::common_type<real>::type n, real d, real rcp_d) {
+  return cl_div_p<real>(c, n, Recip<real>{d, rcp_d});
+}
+template <typename real, typename P>
+CLOUDSC_HD real cl_div_lit_p(const P& c, typename std::common_type<real>::type n, real d) {
+  return cl_div_p<real>(c, n, Recip<real>{d, real(1) / d});
+}
+
 // FOEALFA (src/common/include/fcttre.func.h; inlined at cloudsc_c.c:588,831,1162-1174)
 template <typename real, typename P>
 CLOUDSC_HD real foealfa(const P& c, real t) {
@@ -488,15 +535,15 @@ CLOUDSC_HD real foealfa(const P& c, real t) {
   return fmin(R(1.0), x * x);            // pow(x,2) == x*x (both rounded once)
 }
 template <typename real, typename P>
-CLOUDSC_HD real exp_liq(const P& c, real t) { return cl_exp<real>(c, cl_div<real>(c.r3les * (t - c.rtt), t - c.r4les)); }
+CLOUDSC_HD real exp_liq(const P& c, real t) { return cl_exp<real>(c, cl_div_p<real>(c, c.r3les * (t - c.rtt), t - c.r4les)); }
 template <typename real, typename P>
-CLOUDSC_HD real exp_ice(const P& c, real t) { return cl_exp<real>(c, cl_div<real>(c.r3ies * (t - c.rtt), t - c.r4ies)); }
+CLOUDSC_HD real exp_ice(const P& c, real t) { return cl_exp<real>(c, cl_div_p<real>(c, c.r3ies * (t - c.rtt), t - c.r4ies)); }
 
 // alfa*R5ALVCP/(T-R4LES)^2 + (1-alfa)*R5ALSCP/(T-R4IES)^2 (cloudsc_c.c:1166,1220)
 template <typename real, typename P>
 CLOUDSC_HD real foedem_term(const P& c, real t, real alfa) {
   real dl = t - c.r4les, di = t - c.r4ies;
-  return ((alfa * c.r5alvcp) * cl_div<real>(R(1.0), dl * dl)) + (((R(1.0) - alfa) * c.r5alscp) * cl_div<real>(R(1.0), di * di));
+  return ((alfa * c.r5alvcp) * cl_div_p<real>(c, R(1.0), dl * dl)) + (((R(1.0) - alfa) * c.r5alscp) * cl_div_p<real>(c, R(1.0), di * di));
 }
 
 }  // namespace cloudsc

@@ -315,21 +315,21 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // saturation values (:583-609)
     const real e_liq = exp_liq<real>(c, ztp1), e_ice = exp_ice<real>(c, ztp1);
     // divisors shared by several divisions (cl_recip: one reciprocal, same quotient bits)
-    const Recip<real> r_pap = cl_recip(pap_k);
-    const real zfoeewmt = fmin(cl_div((c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)), r_pap), R(0.5));
-    const Recip<real> r_mixd = cl_recip(R(1.0) - c.retv * zfoeewmt);
-    const real zqsmix = cl_div(zfoeewmt, r_mixd);
+    const Recip<real> r_pap = cl_recip_p<real>(c, pap_k);
+    const real zfoeewmt = fmin(cl_div_p<real>(c, (c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)), r_pap), R(0.5));
+    const Recip<real> r_mixd = cl_recip_p<real>(c, R(1.0) - c.retv * zfoeewmt);
+    const real zqsmix = cl_div_p<real>(c, zfoeewmt, r_mixd);
     const real zalfa_d = fmax(R(0.0), copysign(R(1.0), ztp1 - c.rtt));
-    real zfoeew = fmin(cl_div((zalfa_d * (c.r2es * e_liq) + (R(1.0) - zalfa_d) * (c.r2es * e_ice)), r_pap), R(0.5));
+    real zfoeew = fmin(cl_div_p<real>(c, (zalfa_d * (c.r2es * e_liq) + (R(1.0) - zalfa_d) * (c.r2es * e_ice)), r_pap), R(0.5));
     zfoeew = fmin(R(0.5), zfoeew);
-    const Recip<real> r_iced = cl_recip(R(1.0) - c.retv * zfoeew);
-    const real zqsice = cl_div(zfoeew, r_iced);
+    const Recip<real> r_iced = cl_recip_p<real>(c, R(1.0) - c.retv * zfoeew);
+    const real zqsice = cl_div_p<real>(c, zfoeew, r_iced);
     // (zqsliq, :601-604, is computed where rain evaporation, its only reader, runs)
     // liquid/ice fractions (:628-636)
     const real zli = zqx[QL] + zqx[QI];
     real zliqfrac = R(0.0), zicefrac = R(0.0);
     if (zli > c.rlmin) {
-      zliqfrac = cl_div(zqx[QL], zli);
+      zliqfrac = cl_div_p<real>(c, zqx[QL], zli);
       zicefrac = R(1.0) - zliqfrac;
     }
 
@@ -355,23 +355,23 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     // 3.0 derived variables (:799-841)
     const real zdp = nb.paph_n - nb.paph_k;
-    const real zgdp = cl_div(c.rg, zdp);
-    const real zrho = cl_div(pap_k, (c.rd * ztp1));
+    const real zgdp = cl_div_p<real>(c, c.rg, zdp);
+    const real zrho = cl_div_p<real>(c, pap_k, (c.rd * ztp1));
     const real zdtgdp = c.ptsphy * zgdp;
     const real zrdtgdp = zdp * c.zinv_tsrg;
     real zfacw, zfaci, zfac, zcor;
-    { const real d = ztp1 - c.r4les; zfacw = cl_div(c.r5les, (d * d)); }
-    { const real d = ztp1 - c.r4ies; zfaci = cl_div(c.r5ies, (d * d)); }
-    zcor = cl_div(R(1.0), r_iced);
+    { const real d = ztp1 - c.r4les; zfacw = cl_div_p<real>(c, c.r5les, (d * d)); }
+    { const real d = ztp1 - c.r4ies; zfaci = cl_div_p<real>(c, c.r5ies, (d * d)); }
+    zcor = cl_div_p<real>(c, R(1.0), r_iced);
     const real zdqsicedt = (zfaci * zcor) * zqsice;
     const real zcorqsice = R(1.0) + c.ralsdcp * zdqsicedt;
     zfac = zfoealfa * zfacw + (R(1.0) - zfoealfa) * zfaci;
-    zcor = cl_div(R(1.0), r_mixd);
+    zcor = cl_div_p<real>(c, R(1.0), r_mixd);
     const real zdqsmixdt = (zfac * zcor) * zqsmix;
     const real zcorqsmix = R(1.0) + (zfoealfa * c.ralvdcp + (R(1.0) - zfoealfa) * c.ralsdcp) * zdqsmixdt;
-    const real zevaplimmix = fmax(cl_div((zqsmix - zqx[QV]), zcorqsmix), R(0.0));
-    real ztmpa = cl_div(R(1.0), fmax(za, zepsec));
-    const Recip<real> r_1mza = cl_recip(fmax(zepsec, R(1.0) - za));
+    const real zevaplimmix = fmax(cl_div_p<real>(c, (zqsmix - zqx[QV]), zcorqsmix), R(0.0));
+    real ztmpa = cl_div_p<real>(c, R(1.0), fmax(za, zepsec));
+    const Recip<real> r_1mza = cl_recip_p<real>(c, fmax(zepsec, R(1.0) - za));
     real zliqcld = zqx[QL] * ztmpa;
     real zicecld = zqx[QI] * ztmpa;
     real zlicld = zliqcld + zicecld;
@@ -381,7 +381,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (zqx[QI] < c.rlmin) { sa_iv = zqx[QI]; }
 
     // 3.1 ice supersaturation adjustment (:874-954)
-    const real zfokoop = fmin(c.rkoop1 - c.rkoop2 * ztp1, cl_div((c.r2es * e_liq) * R(1.0), (c.r2es * e_ice)));
+    const real zfokoop = fmin(c.rkoop1 - c.rkoop2 * ztp1, cl_div_p<real>(c, (c.r2es * e_liq) * R(1.0), (c.r2es * e_ice)));
     if (c.nssopt == 0 || ztp1 >= c.rtt) {
       zfac = R(1.0);
       zfaci = R(1.0);
@@ -391,10 +391,10 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
     real zsupsat;
     if (za > c.one_m_ramin) {
-      zsupsat = fmax(cl_div((zqx[QV] - zfac * zqsice), zcorqsice), R(0.0));
+      zsupsat = fmax(cl_div_p<real>(c, (zqx[QV] - zfac * zqsice), zcorqsice), R(0.0));
     } else {
-      const real zqp1env = cl_div((zqx[QV] - za * zqsice), fmax(R(1.0) - za, zepsilon));
-      zsupsat = fmax(cl_div(((R(1.0) - za) * (zqp1env - zfac * zqsice)), zcorqsice), R(0.0));
+      const real zqp1env = cl_div_p<real>(c, (zqx[QV] - za * zqsice), fmax(R(1.0) - za, zepsilon));
+      zsupsat = fmax(cl_div_p<real>(c, ((R(1.0) - za) * (zqp1env - zfac * zqsice)), zcorqsice), R(0.0));
     }
     const bool warm_homo = ztp1 > c.rthomo;
     if (zsupsat > zepsec) {
@@ -416,7 +416,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (k < klev - 1) {
       plude_k = plude_k * zdtgdp;
       if (nb.plu_n > zepsec && plude_k > c.rlmin) {
-        zsolac = zsolac + cl_div(plude_k, nb.plu_n);
+        zsolac = zsolac + cl_div_p<real>(c, plude_k, nb.plu_n);
         conv_src_l = zfoealfa * plude_k;
         conv_src_i = (R(1.0) - zfoealfa) * plude_k;
         sa_ll = sa_ll + conv_src_l;
@@ -435,7 +435,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       const real zlcust_i = zmf * cs.qxnm1_i;
       conv_src_l = conv_src_l + zlcust_l;
       conv_src_i = conv_src_i + zlcust_i;
-      const real zdtdp = cl_div(((c.zrdcp * R(0.5)) * (cs.t_prev + ztp1)), nb.paph_k);
+      const real zdtdp = cl_div_p<real>(c, ((c.zrdcp * R(0.5)) * (cs.t_prev + ztp1)), nb.paph_k);
       const real zdtforc = zdtdp * (pap_k - cs.pap_prev);
       const real zdqs = (cs.zanewm1 * zdtforc) * zdqsmixdt;
       real zlfinalsum = R(0.0);
@@ -473,7 +473,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       real zleros = za * ze;
       zleros = fmin(zleros, zevaplimmix);
       zleros = fmin(zleros, zli);
-      const real zaeros = cl_div(zleros, zlicld);
+      const real zaeros = cl_div_p<real>(c, zleros, zlicld);
       zsolac = zsolac - zaeros;
       sa_lv = sa_lv + zliqfrac * zleros;
       sa_iv = sa_iv + zicefrac * zleros;
@@ -482,7 +482,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // 3.4 condensation/evaporation due to dqsat/dt: two Newton steps (:1137-1182)
     real zdqs;
     {
-      const real zdtdp = cl_div((c.zrdcp * ztp1), r_pap);
+      const real zdtdp = cl_div_p<real>(c, (c.zrdcp * ztp1), r_pap);
       const real zdpmxdt = zdp * c.zqtmst;
       const real zmfdn = (k < klev - 1) ? nb.pmfu_n + nb.pmfd_n : R(0.0);
       real zwtot = in.pvervel + c.half_rg * (nb.pmfu_k + nb.pmfd_k + zmfdn);
@@ -492,15 +492,15 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       const real zdtforc = (zdtdp * zwtot) * c.ptsphy + zdtdiab;
       real tt = fmax(ztp1 + zdtforc, R(160.0));
       real qsm = zqsmix;
-      const real zqp = cl_div(R(1.0), r_pap);
+      const real zqp = cl_div_p<real>(c, R(1.0), r_pap);
   #pragma unroll
       for (int it = 0; it < 2; it++) {
         const real a = foealfa<real>(c, tt);
         real zqsat = (c.r2es * (a * exp_liq<real>(c, tt) + (R(1.0) - a) * exp_ice<real>(c, tt))) * zqp;
         zqsat = fmin(R(0.5), zqsat);
-        const real zcor2 = cl_div(R(1.0), (R(1.0) - c.retv * zqsat));
+        const real zcor2 = cl_div_p<real>(c, R(1.0), (R(1.0) - c.retv * zqsat));
         zqsat = zqsat * zcor2;
-        const real zcond = cl_div((qsm - zqsat), (R(1.0) + (zqsat * zcor2) * foedem_term<real>(c, tt, a)));
+        const real zcond = cl_div_p<real>(c, (qsm - zqsat), (R(1.0) + (zqsat * zcor2) * foedem_term<real>(c, tt, a)));
         tt = tt + (a * c.ralvdcp + (R(1.0) - a) * c.ralsdcp) * zcond;
         qsm = qsm - zcond;
       }
@@ -520,10 +520,10 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       real zlcond1 = fmax(-zdqs, R(0.0));
       real zcdmax;
       if (za > R(0.99)) {
-        const real zcor3 = cl_div(R(1.0), (R(1.0) - c.retv * zqsmix));
-        zcdmax = cl_div((zqx[QV] - zqsmix), (R(1.0) + (zcor3 * zqsmix) * foedem_term<real>(c, ztp1, zfoealfa)));
+        const real zcor3 = cl_div_p<real>(c, R(1.0), (R(1.0) - c.retv * zqsmix));
+        zcdmax = cl_div_p<real>(c, (zqx[QV] - zqsmix), (R(1.0) + (zcor3 * zqsmix) * foedem_term<real>(c, ztp1, zfoealfa)));
       } else {
-        zcdmax = cl_div((zqx[QV] - za * zqsmix), za);
+        zcdmax = cl_div_p<real>(c, (zqx[QV] - za * zqsmix), za);
       }
       zlcond1 = fmax(fmin(zlcond1, zcdmax), R(0.0));
       zlcond1 = za * zlcond1;
@@ -535,14 +535,14 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // 3.4b(2) generation of new clouds (:1253-1363)
     if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) {
       real zrhc = c.ramid;
-      const real zsigk = cl_div(pap_k, cc.paph_sfc);
+      const real zsigk = cl_div_p<real>(c, pap_k, cc.paph_sfc);
       if (zsigk > R(0.8)) {
-        const real s = cl_div_lit((zsigk - R(0.8)), R(0.2));
+        const real s = cl_div_lit_p<real>(c, (zsigk - R(0.8)), R(0.2));
         zrhc = c.ramid + (R(1.0) - c.ramid) * (s * s);
       }
       real zqe = R(0.0);
       if (c.nssopt == 0 || c.nssopt == 1) {
-        zqe = cl_div((zqx[QV] - za * zqsice), r_1mza);
+        zqe = cl_div_p<real>(c, (zqx[QV] - za * zqsice), r_1mza);
         zqe = fmax(R(0.0), zqe);
       } else if (c.nssopt == 2) {
         zqe = zqx[QV];
@@ -551,10 +551,10 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
       const real zfacn = (c.nssopt == 0 || ztp1 >= c.rtt) ? R(1.0) : zfokoop;
       if (zqe >= zqsice * zfacn * zrhc && zqe < zqsice * zfacn) {
-        real zacond = cl_div(-((R(1.0) - za) * zfacn) * zdqs, fmax(R(2.0) * (zfacn * zqsice - zqe), zepsec));
+        real zacond = cl_div_p<real>(c, -((R(1.0) - za) * zfacn) * zdqs, fmax(R(2.0) * (zfacn * zqsice - zqe), zepsec));
         zacond = fmin(zacond, R(1.0) - za);
         real zlcond2 = -(zfacn * zdqs) * R(0.5) * zacond;
-        const real zzdl = cl_div((R(2.0) * (zfacn * zqsice - zqe)), fmax(zepsec, R(1.0) - za));
+        const real zzdl = cl_div_p<real>(c, (R(2.0) * (zfacn * zqsice - zqe)), fmax(zepsec, R(1.0) - za));
         if (zdqs * zfacn < -zzdl) {
           const real zlcondlim = ((za - R(1.0)) * zfacn) * zdqs - zfacn * zqsice + zqx[QV];
           zlcond2 = fmin(zlcond2, zlcondlim);
@@ -574,26 +574,26 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     // 3.7 growth of ice by vapour deposition, Rotstayn (:1382-1447)
     if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
-    else cs.zcldtopdist = cs.zcldtopdist + cl_div(zdp, (zrho * c.rg));
+    else cs.zcldtopdist = cs.zcldtopdist + cl_div_p<real>(c, zdp, (zrho * c.rg));
     if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
-      const real zvpice = cl_div_known(((c.r2es * e_ice) * c.rv), c.rd, c.rd_rcp);
+      const real zvpice = cl_div_known_p<real>(c, ((c.r2es * e_ice) * c.rv), c.rd, c.rd_rcp);
       const real zvpliq = zvpice * zfokoop;
-      const real zicenuclei = R(1000.0) * cl_exp<real>(c, cl_div((R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
-      const real zadd = cl_div((c.rlstt * (cl_div(c.rlstt, (c.rv * ztp1)) - R(1.0))), (R(0.024) * ztp1));
-      const real zbdd = cl_div(((c.rv * ztp1) * pap_k), (R(2.21) * zvpice));
-      const real zcvds = cl_div(((R(7.8) * cl_pow<real>(c, cl_div(zicenuclei, zrho), R(0.666))) * (zvpliq - zvpice)), ((R(8.87) * (zadd + zbdd)) * zvpice));
-      const real zice0 = fmax(zicecld, cl_div((zicenuclei * c.riceinit), zrho));
+      const real zicenuclei = R(1000.0) * cl_exp<real>(c, cl_div_p<real>(c, (R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
+      const real zadd = cl_div_p<real>(c, (c.rlstt * (cl_div_p<real>(c, c.rlstt, (c.rv * ztp1)) - R(1.0))), (R(0.024) * ztp1));
+      const real zbdd = cl_div_p<real>(c, ((c.rv * ztp1) * pap_k), (R(2.21) * zvpice));
+      const real zcvds = cl_div_p<real>(c, ((R(7.8) * cl_pow<real>(c, cl_div_p<real>(c, zicenuclei, zrho), R(0.666))) * (zvpliq - zvpice)), ((R(8.87) * (zadd + zbdd)) * zvpice));
+      const real zice0 = fmax(zicecld, cl_div_p<real>(c, (zicenuclei * c.riceinit), zrho));
       const real zinew = cl_pow<real>(c, (R(0.666) * zcvds) * c.ptsphy + cl_pow<real>(c, zice0, R(0.666)), R(1.5));
       real zdepos = fmax(za * (zinew - zice0), R(0.0));
       zdepos = fmin(zdepos, zqxfg[QL]);
-      const real zinfactor = fmin(cl_div_lit(zicenuclei, R(15000.0)), R(1.0));
-      zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cl_div_known(cs.zcldtopdist, c.rdepliqrefdepth, c.rdepliqrefdepth_rcp)), R(1.0));
+      const real zinfactor = fmin(cl_div_lit_p<real>(c, zicenuclei, R(15000.0)), R(1.0));
+      zdepos = zdepos * fmin(zinfactor + (R(1.0) - zinfactor) * (c.rdepliqrefrate + cl_div_known_p<real>(c, cs.zcldtopdist, c.rdepliqrefdepth, c.rdepliqrefdepth_rcp)), R(1.0));
       sa_li = sa_li + zdepos;
       zqxfg[QI] = zqxfg[QI] + zdepos; zqxfg[QL] = zqxfg[QL] - zdepos;
     }
 
     // 4. revise in-cloud condensate (:1528-1533)
-    ztmpa = cl_div(R(1.0), fmax(za, zepsec));
+    ztmpa = cl_div_p<real>(c, R(1.0), fmax(za, zepsec));
     zliqcld = zqxfg[QL] * ztmpa;
     zicecld = zqxfg[QI] * ztmpa;
     zlicld = zliqcld + zicecld;
@@ -612,11 +612,11 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // precip cover overlap, MAX-RAN (:1594-1611)
     real zcovpclr, zraincld, zsnowcld;
     if (zqpretot > zepsec) {
-      cs.zcovptot = R(1.0) - cl_div((R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)), (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6))));
+      cs.zcovptot = R(1.0) - cl_div_p<real>(c, (R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)), (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6))));
       cs.zcovptot = fmax(cs.zcovptot, c.rcovpmin);
       zcovpclr = fmax(R(0.0), cs.zcovptot - za);
-      zraincld = cl_div(zqxfg[QR], cs.zcovptot);
-      zsnowcld = cl_div(zqxfg[QS], cs.zcovptot);
+      zraincld = cl_div_p<real>(c, zqxfg[QR], cs.zcovptot);
+      zsnowcld = cl_div_p<real>(c, zqxfg[QS], cs.zcovptot);
       cs.zcovpmax = fmax(cs.zcovptot, cs.zcovpmax);
     } else {
       zraincld = R(0.0); zsnowcld = R(0.0); cs.zcovptot = R(0.0); zcovpclr = R(0.0); cs.zcovpmax = R(0.0);
@@ -629,9 +629,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       real zlcrit = pval(c, c.rlcritsnow);
       if (c.laericeauto) {
         zlcrit = in.picrit_aer;
-        zzco = zzco * cl_pow<real>(c, cl_div(c.rnice, in.pnice), R(0.333));
+        zzco = zzco * cl_pow<real>(c, cl_div_p<real>(c, c.rnice, in.pnice), R(0.333));
       }
-      const real r = cl_div(zicecld, zlcrit);
+      const real r = cl_div_p<real>(c, zicecld, zlcrit);
       sb_is = sb_is + zzco * (R(1.0) - cl_exp<real>(c, -(r * r)));
     }
     // 4.3b warm rain, Khairoutdinov and Kogan 2000 (:1644-1761)
@@ -653,7 +653,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
     // riming of snow by cloud water (:1768-1808)
     if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) {
-      const real zfallcorr = cl_pow<real>(c, cl_div(c.rdensref, zrho), R(0.4));
+      const real zfallcorr = cl_pow<real>(c, cl_div_p<real>(c, c.rdensref, zrho), R(0.4));
       real zsnowrime = ((((R(0.3) * cs.zcovptot) * c.ptsphy) * c.rcl_const7s) * zfallcorr) *
                        cl_pow<real>(c, (zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
       zsnowrime = fmin(zsnowrime, R(1.0));
@@ -665,17 +665,17 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (zicetot > zepsec && ztp1 > c.rtt) {
       const real zsubsat = fmax(zqsice - zqx[QV], R(0.0));
       const real ztdmtw0 = ztp1 - c.rtt - zsubsat * (ztw1 + ztw2 * (pap_k - ztw3) - ztw4 * (ztp1 - ztw5));
-      const real zcons1 = fabs(cl_div_known((c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)), c.rtaumel, c.rtaumel_rcp));
+      const real zcons1 = fabs(cl_div_known_p<real>(c, (c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)), c.rtaumel, c.rtaumel_rcp));
       const real zmeltmax = fmax((ztdmtw0 * zcons1) * c.zrldcp, R(0.0));
       if (zmeltmax > zepsec) {
         {   // ice -> rain
-          const real zalfa = cl_div(zqxfg[QI], zicetot);
+          const real zalfa = cl_div_p<real>(c, zqxfg[QI], zicetot);
           const real zmelt = fmin(zqxfg[QI], zalfa * zmeltmax);
           zqxfg[QI] = zqxfg[QI] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
           sa_ir = sa_ir + zmelt;
         }
         {   // snow -> rain
-          const real zalfa = cl_div(zqxfg[QS], zicetot);
+          const real zalfa = cl_div_p<real>(c, zqxfg[QS], zicetot);
           const real zmelt = fmin(zqxfg[QS], zalfa * zmeltmax);
           zqxfg[QS] = zqxfg[QS] - zmelt; zqxfg[QR] = zqxfg[QR] + zmelt;
           sa_sr = sa_sr + zmelt;
@@ -687,17 +687,17 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (zqx[QR] > zepsec) {
       if (cold && cs.t_prev > c.rtt) {
         const real tot = fmax(zqx[QS] + zqx[QR], zepsec);
-        cs.rainfrac = cl_div(zqx[QR], tot);
+        cs.rainfrac = cl_div_p<real>(c, zqx[QR], tot);
       }
       if (ztp1 < c.rtt) {
         real zfrzmax;
         if (cs.rainfrac > R(0.8)) {
-          const real zlambda = cl_pow<real>(c, cl_div(c.rcl_fac1, (zrho * zqx[QR])), c.rcl_fac2);
+          const real zlambda = cl_pow<real>(c, cl_div_p<real>(c, c.rcl_fac1, (zrho * zqx[QR])), c.rcl_fac2);
           const real ztemp = c.rcl_fzrab * (ztp1 - c.rtt);
-          const real zfrz = ((c.ptsphy * (cl_div(c.rcl_const5r, zrho))) * (cl_exp<real>(c, ztemp) - R(1.0))) * cl_pow<real>(c, zlambda, c.rcl_const6r);
+          const real zfrz = ((c.ptsphy * (cl_div_p<real>(c, c.rcl_const5r, zrho))) * (cl_exp<real>(c, ztemp) - R(1.0))) * cl_pow<real>(c, zlambda, c.rcl_const6r);
           zfrzmax = fmax(zfrz, R(0.0));
         } else {
-          const real zcons1 = fabs(cl_div_known((c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))), c.rtaumel, c.rtaumel_rcp));
+          const real zcons1 = fabs(cl_div_known_p<real>(c, (c.ptsphy * (R(1.0) + R(0.5) * (c.rtt - ztp1))), c.rtaumel, c.rtaumel_rcp));
           zfrzmax = fmax(((c.rtt - ztp1) * zcons1) * c.zrldcp, R(0.0));
         }
         if (zfrzmax > zepsec) {
@@ -720,47 +720,47 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // inside the precipitation tests that guard their only uses, so a wave
     // without rain or snow skips their divisions.  Same operations, same bits.
     auto zzrh0_of = [&]() {
-      return fmin(fmax(c.rprecrhmax + cl_div(((R(1.0) - c.rprecrhmax) * cs.zcovpmax), r_1mza), c.rprecrhmax), R(1.0));
+      return fmin(fmax(c.rprecrhmax + cl_div_p<real>(c, ((R(1.0) - c.rprecrhmax) * cs.zcovpmax), r_1mza), c.rprecrhmax), R(1.0));
     };
     if (zcovpclr > zepsec && zqxfg[QR] > zepsec) {
-      const real zfoeeliqt = fmin(cl_div((c.r2es * e_liq), r_pap), R(0.5));
-      const real zqsliq = cl_div(zfoeeliqt, (R(1.0) - c.retv * zfoeeliqt));
+      const real zfoeeliqt = fmin(cl_div_p<real>(c, (c.r2es * e_liq), r_pap), R(0.5));
+      const real zqsliq = cl_div_p<real>(c, zfoeeliqt, (R(1.0) - c.retv * zfoeeliqt));
       const real zzrh = fmin(R(0.8), zzrh0_of());
       const real zqe = fmax(R(0.0), fmin(zqx[QV], zqsliq));
       if (zqe < zzrh * zqsliq) {
-        const real zpreclr = cl_div(zqxfg[QR], cs.zcovptot);
-        const real zfallcorr = cl_pow<real>(c, cl_div(c.rdensref, zrho), R(0.4));
+        const real zpreclr = cl_div_p<real>(c, zqxfg[QR], cs.zcovptot);
+        const real zfallcorr = cl_pow<real>(c, cl_div_p<real>(c, c.rdensref, zrho), R(0.4));
         const real zesatliq = c.rv_rd * (c.r2es * e_liq);
-        const real zlambda = cl_pow<real>(c, cl_div(c.rcl_fac1, (zrho * zpreclr)), c.rcl_fac2);
+        const real zlambda = cl_pow<real>(c, cl_div_p<real>(c, c.rcl_fac1, (zrho * zpreclr)), c.rcl_fac2);
         const real zevap_denom = c.rcl_cdenom1 * zesatliq - c.rcl_cdenom2 * ztp1 * zesatliq + (c.rcl_cdenom3 * cl_pow<real>(c, ztp1, R(3.0))) * pap_k;
-        const real zcorr2 = cl_div((cl_pow<real>(c, cl_div_lit(ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
+        const real zcorr2 = cl_div_p<real>(c, (cl_pow<real>(c, cl_div_lit_p<real>(c, ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
         const real zsubsat = fmax(zzrh * zqsliq - zqe, R(0.0));
-        const real zbeta = ((((cl_div(R(0.5), zqsliq)) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (cl_div(zcorr2, zevap_denom)) *
-                           (cl_div(R(0.78), cl_pow<real>(c, zlambda, c.rcl_const4r)) + cl_div((c.rcl_const2r * sqrt(zrho * zfallcorr)), (sqrt(zcorr2) * cl_pow<real>(c, zlambda, c.rcl_const3r))));
+        const real zbeta = ((((cl_div_p<real>(c, R(0.5), zqsliq)) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (cl_div_p<real>(c, zcorr2, zevap_denom)) *
+                           (cl_div_p<real>(c, R(0.78), cl_pow<real>(c, zlambda, c.rcl_const4r)) + cl_div_p<real>(c, (c.rcl_const2r * sqrt(zrho * zfallcorr)), (sqrt(zcorr2) * cl_pow<real>(c, zlambda, c.rcl_const3r))));
         const real zdenom = R(1.0) + zbeta * c.ptsphy;
-        const real zdpevap = cl_div((((zcovpclr * zbeta) * c.ptsphy) * zsubsat), zdenom);
+        const real zdpevap = cl_div_p<real>(c, (((zcovpclr * zbeta) * c.ptsphy) * zsubsat), zdenom);
         const real zevap = fmin(zdpevap, zqxfg[QR]);
         sa_rv = sa_rv + zevap;
-        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), cl_div(((cs.zcovptot - za) * zevap), zqxfg[QR])));
+        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), cl_div_p<real>(c, ((cs.zcovptot - za) * zevap), zqxfg[QR])));
         zqxfg[QR] = zqxfg[QR] - zevap;
       }
     }
     // 4.5 evaporation of snow, Sundqvist (:2048-2087)
     if (zcovpclr > zepsec && zqxfg[QS] > zepsec) {
       const real zzrh = zzrh0_of();
-      real zqe = cl_div((zqx[QV] - za * zqsice), r_1mza);
+      real zqe = cl_div_p<real>(c, (zqx[QV] - za * zqsice), r_1mza);
       zqe = fmax(R(0.0), fmin(zqe, zqsice));
       if (zqe < zzrh * zqsice) {
         const real x = cs.zcovptot * zdtgdp;
-        const real zpreclr = cl_div((zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
-        const real zbeta1 = cl_div(((cl_div_known(sqrt(cl_div(pap_k, cc.paph_sfc)), c.rvrfactor, c.rvrfactor_rcp)) * zpreclr), fmax(zcovpclr, zepsec));
+        const real zpreclr = cl_div_p<real>(c, (zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
+        const real zbeta1 = cl_div_p<real>(c, ((cl_div_known_p<real>(c, sqrt(cl_div_p<real>(c, pap_k, cc.paph_sfc)), c.rvrfactor, c.rvrfactor_rcp)) * zpreclr), fmax(zcovpclr, zepsec));
         const real zbeta = c.rg_rpecons * cl_pow<real>(c, zbeta1, R(0.5777));
         const real zdenom = R(1.0) + (zbeta * c.ptsphy) * zcorqsice;
-        const real zdpr = ((cl_div(((zcovpclr * zbeta) * (zqsice - zqe)), zdenom)) * zdp) * c.zrg_r;
+        const real zdpr = ((cl_div_p<real>(c, ((zcovpclr * zbeta) * (zqsice - zqe)), zdenom)) * zdp) * c.zrg_r;
         const real zdpevap = zdpr * zdtgdp;
         const real zevap = fmin(zdpevap, zqxfg[QS]);
         sa_sv = sa_sv + zevap;
-        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), cl_div(((cs.zcovptot - za) * zevap), zqxfg[QS])));
+        cs.zcovptot = fmax(c.rcovpmin, cs.zcovptot - fmax(R(0.0), cl_div_p<real>(c, ((cs.zcovptot - za) * zevap), zqxfg[QS])));
         zqxfg[QS] = zqxfg[QS] - zevap;
       }
     }
@@ -769,7 +769,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     if (zqxfg[QS] < c.rlmin) { sa_sv = sa_sv + zqxfg[QS]; }
 
     // 5.1 cloud cover (:2168-2180)
-    real zanew = cl_div((za + zsolac), (R(1.0) + zsolab));
+    real zanew = cl_div_p<real>(c, (za + zsolac), (R(1.0) + zsolab));
     zanew = fmin(zanew, R(1.0));
     if (zanew < c.ramin) zanew = R(0.0);
     const real zda = zanew - zaorig;
@@ -796,7 +796,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       {
         const real zmm = fmax(zqx[QL], zepsec), den = fmax(R(0.0) - psum, zmm);
         if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
-          zrat = cl_div(zmm, den);
+          zrat = cl_div_p<real>(c, zmm, den);
           if (sa_ll < R(0.0)) { sa_ll = sa_ll * zrat; sa_ll = sa_ll * zrat; }
           if (-sa_li < R(0.0)) sa_li = sa_li * zrat;
           if (-sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
@@ -809,7 +809,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       {
         const real zmm = fmax(zqx[QI], zepsec), den = fmax(R(0.0) - psum, zmm);
         if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
-          zrat = cl_div(zmm, den);
+          zrat = cl_div_p<real>(c, zmm, den);
           if (sa_li < R(0.0)) sa_li = sa_li * zrat;
           if (sa_ii < R(0.0)) { sa_ii = sa_ii * zrat; sa_ii = sa_ii * zrat; }
           if (-sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
@@ -821,7 +821,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       {
         const real zmm = fmax(zqx[QR], zepsec), den = fmax(R(0.0) - psum, zmm);
         if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
-          zrat = cl_div(zmm, den);
+          zrat = cl_div_p<real>(c, zmm, den);
           if (sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
           if (sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
           if (sa_rr < R(0.0)) { sa_rr = sa_rr * zrat; sa_rr = sa_rr * zrat; }
@@ -834,7 +834,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       {
         const real zmm = fmax(zqx[QS], zepsec), den = fmax(R(0.0) - psum, zmm);
         if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
-          zrat = cl_div(zmm, den);
+          zrat = cl_div_p<real>(c, zmm, den);
           if (sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
           if (-sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
           if (sa_ss < R(0.0)) { sa_ss = sa_ss * zrat; sa_ss = sa_ss * zrat; }
@@ -846,7 +846,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       {
         const real zmm = fmax(zqx[QV], zepsec), den = fmax(R(0.0) - psum, zmm);
         if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
-          zrat = cl_div(zmm, den);
+          zrat = cl_div_p<real>(c, zmm, den);
           if (sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
           if (sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
           if (sa_rv < R(0.0)) sa_rv = sa_rv * zrat;
@@ -884,19 +884,19 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       const real d_s = R(1.0) + fsink_s;
       // off-diagonals zqlhs[ql][qs] = -sb_ls, zqlhs[qi][qs] = -sb_is; LU scales row-wise by
       // the pivot of the eliminating column: zqlhs[n][m] /= zqlhs[n][n] for m > n.
-      const Recip<real> r_dl = cl_recip(d_l), r_di = cl_recip(d_i);
-      const real u_ls = cl_div((-sb_ls), r_dl);    // zqlhs[ql][qs] after jn = ql
-      const real u_is = cl_div((-sb_is), r_di);    // zqlhs[qi][qs] after jn = qi
+      const Recip<real> r_dl = cl_recip_p<real>(c, d_l), r_di = cl_recip_p<real>(c, d_i);
+      const real u_ls = cl_div_p<real>(c, (-sb_ls), r_dl);    // zqlhs[ql][qs] after jn = ql
+      const real u_is = cl_div_p<real>(c, (-sb_is), r_di);    // zqlhs[qi][qs] after jn = qi
       // forward substitution (step 1): zqxn[qs] -= zqlhs[ql][qs]*zqxn[ql] + zqlhs[qi][qs]*zqxn[qi]
       qn_s = qn_s - u_ls * qn_l;
       qn_s = qn_s - u_is * qn_i;
       // back substitution (step 2): vapour and the diagonal solves
       // qn_v = qn_v / zqlhs[qv][qv] with a pivot of exactly 1: x / 1 == x in IEEE arithmetic
       // (signed zeros and NaN included), so the division is dropped
-      qn_s = cl_div(qn_s, d_s);
-      qn_r = cl_div(qn_r, d_r);
-      qn_i = cl_div(qn_i, r_di);
-      qn_l = cl_div(qn_l, r_dl);
+      qn_s = cl_div_p<real>(c, qn_s, d_s);
+      qn_r = cl_div_p<real>(c, qn_r, d_r);
+      qn_i = cl_div_p<real>(c, qn_i, r_di);
+      qn_l = cl_div_p<real>(c, qn_l, r_dl);
       // no small values (:2402-2412)
       if (qn_l < zepsec) { qn_v = qn_v + qn_l; qn_l = R(0.0); }
       if (qn_i < zepsec) { qn_v = qn_v + qn_i; qn_i = R(0.0); }

@@ -2,6 +2,7 @@
 // (cloudsc_state_*): on-device expansion of the KLON-column template (g % klon
 // of the GLOBAL column index), timed runs on the state's stream, and on-device
 // validation statistics against the KLON-column reference.
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -135,10 +136,34 @@ void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
   return slots[id];
 }
 
+// diagnostic allocation flags of the state's fields (cloudsc_debug_set_state_layout)
+std::atomic<unsigned> g_alloc_flags{0};
+
 int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
-  hipError_t e = hipMalloc(p, bytes);
+  const unsigned fl = g_alloc_flags.load();
+  hipError_t e = fl ? hipExtMallocWithFlags(p, bytes, fl) : hipMalloc(p, bytes);
   if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
   s->allocs.push_back(*p);
+  return CLOUDSC_OK;
+}
+
+// Diagnostic field placement (cloudsc_debug_set_state_layout): < 0 = one
+// hipMalloc per field (the default); >= 0 = all fields of a state carved out of
+// one arena, field i starting at a 2 MiB boundary plus (i * stagger) mod 2 MiB.
+std::atomic<long long> g_layout_stagger{-1};
+constexpr size_t kArenaAlign = (size_t)2 << 20;
+struct Arena {
+  char* base = nullptr;
+  size_t off = 0;
+  long long stagger = -1;
+  int n = 0;
+};
+size_t arena_span(size_t bytes) { return (bytes + kArenaAlign - 1) / kArenaAlign * kArenaAlign + kArenaAlign; }
+int field_alloc(cloudsc_gpu_state* s, Arena& ar, void** p, size_t bytes) {
+  if (!ar.base) return dalloc(s, p, bytes);
+  *p = ar.base + ar.off + (size_t)(((long long)ar.n * ar.stagger) % (long long)kArenaAlign);
+  ar.off += arena_span(bytes);
+  ar.n++;
   return CLOUDSC_OK;
 }
 
@@ -225,28 +250,45 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
       {&f.pre_ice, t->pre_ice, kl, n2, false}, {&f.pccn, t->pccn, kl, n2, false}, {&f.pnice, t->pnice, kl, n2, false},
       {(const void**)&plude_dev, t->plude, kl, n2, false},
   };
-  for (In& in : ins) {
-    if (!in.src) continue;
-    void* p = nullptr;
-    if ((rc = dalloc(s, &p, in.bytes))) return fail(rc);
-    if ((rc = expand_into(s, p, in.src, in.nlev, in.is_int))) return fail(rc);
-    *in.dst = p;
-  }
-  s->plude_pristine = plude_dev;
   struct Out { void** dst; size_t bytes; };
   Out outs[] = {{&f.plude, n2}, {&f.tendency_loc_t, n2}, {&f.tendency_loc_q, n2}, {&f.tendency_loc_a, n2},
                 {&f.tendency_loc_cld, n3}, {&f.pcovptot, n2}, {&f.prainfrac_toprfz, n1},
                 {&f.pfsqlf, n2h}, {&f.pfsqif, n2h}, {&f.pfcqnng, n2h}, {&f.pfcqlng, n2h}, {&f.pfsqrf, n2h},
                 {&f.pfsqsf, n2h}, {&f.pfcqrng, n2h}, {&f.pfcqsng, n2h}, {&f.pfsqltur, n2h}, {&f.pfsqitur, n2h},
                 {&f.pfplsl, n2h}, {&f.pfplsn, n2h}, {&f.pfhpsl, n2h}, {&f.pfhpsn, n2h}};
+  Arena ar;
+  ar.stagger = g_layout_stagger.load();
+  if (ar.stagger >= 0) {
+    size_t total = 0;
+    for (const In& in : ins)
+      if (in.src) total += arena_span(in.bytes);
+    for (const Out& o : outs) total += arena_span(o.bytes);
+    void* base = nullptr;
+    if ((rc = dalloc(s, &base, total))) return fail(rc);
+    ar.base = (char*)base;
+  }
+  for (In& in : ins) {
+    if (!in.src) continue;
+    void* p = nullptr;
+    if ((rc = field_alloc(s, ar, &p, in.bytes))) return fail(rc);
+    if ((rc = expand_into(s, p, in.src, in.nlev, in.is_int))) return fail(rc);
+    *in.dst = p;
+  }
+  s->plude_pristine = plude_dev;
   for (Out& o : outs) {
-    if ((rc = dalloc(s, o.dst, o.bytes))) return fail(rc);
+    if ((rc = field_alloc(s, ar, o.dst, o.bytes))) return fail(rc);
     if (hipMemsetAsync(*o.dst, 0xff, o.bytes, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);  // NaN
   }
   if (hipMemcpyAsync(f.plude, s->plude_pristine, n2, hipMemcpyDeviceToDevice, s->stream) != hipSuccess)
     return fail(CLOUDSC_EHIP);
   if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);
   *out = s;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags) {
+  g_layout_stagger.store(stagger < 0 ? -1 : stagger);
+  g_alloc_flags.store(alloc_flags);
   return CLOUDSC_OK;
 }
 

@@ -75,10 +75,12 @@ extern "C" {
 /* Option bit, OR-ed into a `variant` argument (cloudsc_gpu_run, cloudsc_state_run,
  * cloudsc_host_pipeline_run).  fp32 evaluates exp/pow in single precision with
  * the device's float forms by default (hardware exp2/log2 with an exact
- * argument reduction: <= 2 ulp, every operation float); with this bit it uses
- * the reference CPU build's glibc expf/powf algorithms instead (computed in
- * double, bit-identical to the single-precision restatement, slower).  fp64
- * always uses the reference CPU build's exp/pow and ignores the bit. */
+ * argument reduction: <= 2 ulp, every operation float) and divides with the
+ * hardware reciprocal and one residual correction (within 1 ulp); with this
+ * bit it uses the reference CPU build's glibc expf/powf algorithms (computed in
+ * double) and correctly rounded divisions instead: bit-identical to the
+ * single-precision restatement, slower.  fp64 always uses the reference CPU
+ * build's exp/pow and IEEE divisions and ignores the bit. */
 #define CLOUDSC_FP32_EXACT_LIBM 0x100
 
 /* error codes */
@@ -156,7 +158,8 @@ int cloudsc_gpu_device_count(int *count);
  * cloudsc_gpu_run.  Calling it again replaces the set in place: it first waits
  * for all work on the device (hipDeviceSynchronize), so launches already
  * queued keep the parameters they were launched with.  States and host
- * pipelines are not affected (they hold their own copy). */
+ * pipelines are not affected (they hold their own copy).  Not to be called
+ * concurrently with launches on the same device (see the top of this file). */
 int cloudsc_gpu_init(int device, const cloudsc_params_t *params);
 
 /* Enqueue one CLOUDSC step over ngptot columns on `stream` (a hipStream_t, or
@@ -201,6 +204,15 @@ int cloudsc_debug_set_kseg_spin_limit(long long limit);
  * The result bits do not depend on either; the tests use it to exercise the
  * hand-offs with few workgroups and many segments. */
 int cloudsc_debug_set_kseg_schedule(int nseg, int grid);
+
+/* Diagnostic: field placement of the states created after this call.  < 0 (the
+ * default): one device allocation per field.  >= 0: all fields of a state in
+ * one allocation, field i starting at a 2 MiB boundary plus (i * stagger) mod
+ * 2 MiB -- for measuring how the HBM placement of the ~47 concurrently
+ * streamed fields affects the kernel time (tools/ab_layout.py).  alloc_flags:
+ * 0 = hipMalloc, else hipExtMallocWithFlags with these flags (e.g. 4 =
+ * hipDeviceMallocContiguous) for the state's field allocations. */
+int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags);
 
 /* Diagnostic: the kernels' single-precision exp/pow on the device, element-wise
  * over n host values: which = 0 the float-internal expf (CLOUDSC_FP32 default),
