@@ -12,7 +12,7 @@
 // Every configuration is allocated `reps` times (fresh memory each time) and
 // timed (best of 5 launches after a warm-up) to show the spread.
 //
-//   ./membench4 <layout 0|1|2> <contiguous 0|1> [reps 3] [len 0] [ngptot 163840]
+//   ./membench4 <layout 0|1|2> <contiguous 0|1> [reps 3] [len 0] [ngptot 163840] [nt 1]
 // build: hipcc --offload-arch=gfx950 -O3 tools/membench4.hip -o build/membench4
 #include <hip/hip_runtime.h>
 
@@ -37,6 +37,7 @@ struct Layout {
   long long bstride, kstride;   // elements between blocks / levels of one field
 };
 
+template <bool NT>
 __global__ void __launch_bounds__(64) persistent(Layout p, int klev, int nblocks, unsigned* counter, int len) {
   extern __shared__ double pad[];
   __shared__ int s_item;
@@ -59,7 +60,8 @@ __global__ void __launch_bounds__(64) persistent(Layout p, int klev, int nblocks
       double v[NIN];
 #pragma unroll
       for (int f = 0; f < NIN; f++)
-        v[f] = __builtin_nontemporal_load((const double*)((const char*)(p.in[f] + u) + lo));
+        v[f] = NT ? __builtin_nontemporal_load((const double*)((const char*)(p.in[f] + u) + lo))
+                  : *(const double*)((const char*)(p.in[f] + u) + lo);
       double s = carry;
 #pragma unroll
       for (int f = 0; f < NIN; f++) s += v[f];
@@ -67,7 +69,8 @@ __global__ void __launch_bounds__(64) persistent(Layout p, int klev, int nblocks
       for (int n = 0; n < len; n++) s = __builtin_fma(s, 0.999999, v[n & 7]);
 #pragma unroll
       for (int f = 0; f < NOUT; f++)
-        __builtin_nontemporal_store(s + f, (double*)((char*)(p.out[f] + u) + lo));
+        if (NT) __builtin_nontemporal_store(s + f, (double*)((char*)(p.out[f] + u) + lo));
+        else *(double*)((char*)(p.out[f] + u) + lo) = s + f;
       carry = s * 1e-3;
     }
   }
@@ -80,6 +83,7 @@ int main(int argc, char** argv) {
   const int reps = argc > 3 ? atoi(argv[3]) : 3;
   const int len = argc > 4 ? atoi(argv[4]) : 0;
   const int ngptot = argc > 5 ? atoi(argv[5]) : 163840;
+  const int nt = argc > 6 ? atoi(argv[6]) : 1;   // non-temporal loads and stores (the kernel's policy)
   const int klev = 137, nblocks = ngptot / 64, wps = 2;
   const size_t plane = (size_t)nblocks * klev * 64;
   const size_t two_mb = (size_t)2 << 20;
@@ -135,9 +139,11 @@ int main(int argc, char** argv) {
         // both arenas use NIN fields per level (outputs padded to NIN planes).
         Layout q = p;
         q.bstride = (long long)klev * NIN * 64; q.kstride = (long long)NIN * 64;
-        hipLaunchKernelGGL(persistent, dim3(grid), dim3(64), lds, 0, q, klev, nblocks, counter, len);
+        if (nt) hipLaunchKernelGGL(persistent<true>, dim3(grid), dim3(64), lds, 0, q, klev, nblocks, counter, len);
+        else hipLaunchKernelGGL(persistent<false>, dim3(grid), dim3(64), lds, 0, q, klev, nblocks, counter, len);
       } else {
-        hipLaunchKernelGGL(persistent, dim3(grid), dim3(64), lds, 0, p, klev, nblocks, counter, len);
+        if (nt) hipLaunchKernelGGL(persistent<true>, dim3(grid), dim3(64), lds, 0, p, klev, nblocks, counter, len);
+        else hipLaunchKernelGGL(persistent<false>, dim3(grid), dim3(64), lds, 0, p, klev, nblocks, counter, len);
       }
       CHK(hipEventRecord(e1));
       CHK(hipEventSynchronize(e1));
@@ -146,8 +152,8 @@ int main(int argc, char** argv) {
       if (rep > 0 && ms < best) best = ms;
     }
     const double bytes = (double)ngptot * klev * (NIN + NOUT) * 8.0;
-    printf("{\"layout\": %d, \"contiguous\": %d, \"replica\": %d, \"len\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", layout,
-           contig, r, len, best, bytes / (best * 1e-3) / 1e12);
+    printf("{\"layout\": %d, \"contiguous\": %d, \"nt\": %d, \"replica\": %d, \"len\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n",
+           layout, contig, nt, r, len, best, bytes / (best * 1e-3) / 1e12);
     fflush(stdout);
     for (double* d : bufs) CHK(hipFree(d));
   }
