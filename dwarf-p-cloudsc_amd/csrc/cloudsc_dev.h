@@ -302,25 +302,27 @@ inline float cl_exp_host(float x) { return cloudsc_libm::expf_split(x, cloudsc_l
 // hardware log2 (v_log_f32) plus the exponent, y*log2(x) as a float-float
 // (products split with fma, TwoSum), then the same exp2 + ldexp.  Every
 // operation is float (2-cycle issue on gfx950, against 4 for the double
-// internals of glibc's forms); the arguments outside the hot range go to the
-// complete glibc functions (cold).  Accuracy: tests/test_gpu_parity.py
-// (test_fp32_fast_libm_ulp) measures <= 2 ulp against the glibc forms over the
-// argument ranges CLOUDSC uses.
-__device__ __forceinline__ float cl_expf_fast(float x) {
-  if (__builtin_expect(!(__builtin_fabsf(x) < 88.0f), 0)) return cl_expf_cold(x);
+// internals of glibc's forms).  No out-of-line calls: the special cases are
+// branch-free (expf: the argument clamped to [-104, 89], where ldexp over- and
+// underflows to +inf / 0 as expf does, NaN passed through; powf: the exponent
+// clamped likewise, a zero base gives 0 or +inf) -- a call site in the level
+// loop costs the register allocation 5 % of the fp32 kernel time even when it
+// is never taken (profiles/r03/experiment_fp32_nocold_ab.txt).  Accuracy:
+// tests/test_gpu_parity.py (test_fp32_fast_libm_ulp) measures <= 2 ulp against
+// the glibc forms over the argument ranges CLOUDSC uses.
+__device__ __forceinline__ float cl_expf_fast(float x0) {
+  // |x| clamped: e^89 overflows to +inf and e^-104 underflows to 0 through ldexp as they should
+  const float x = __builtin_fminf(__builtin_fmaxf(x0, -104.0f), 89.0f);
   const float kL2e = 0x1.715476p+0f, kL2eLo = 0x1.4ae0bep-26f;   // log2(e) = kL2e + kL2eLo (+ O(2^-50))
   const float ph = x * kL2e;
   float pl = __builtin_fmaf(x, kL2e, -ph);                         // exact: x*kL2e = ph + pl
   pl = __builtin_fmaf(x, kL2eLo, pl);
   const float e = __builtin_rintf(ph);
   const float f = (ph - e) + pl;                                    // |f| <= 1/2 + tiny
-  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)e);
+  const float r = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)e);
+  return x0 != x0 ? x0 : r;                                         // NaN stays NaN
 }
 __device__ __forceinline__ float cl_powf_fast(float x, float y) {
-  const uint32_t ix = __builtin_bit_cast(uint32_t, x), iy = __builtin_bit_cast(uint32_t, y);
-  // hot range: x a positive normal number, y finite and non-zero (else the complete function)
-  if (__builtin_expect(ix - 0x00800000u >= 0x7f800000u - 0x00800000u || 2 * iy - 1 >= 2u * 0x7f800000u - 1, 0))
-    return cl_powf_cold(x, y);
   const float m = __builtin_amdgcn_frexp_mantf(x);                 // x = m * 2^E, m in [1/2, 1)
   const float E = (float)__builtin_amdgcn_frexp_expf(x);
   const float l = __builtin_amdgcn_logf(m);                         // log2(m), in [-1, 0)
@@ -328,10 +330,13 @@ __device__ __forceinline__ float cl_powf_fast(float x, float y) {
   const float b = y * l, b_lo = __builtin_fmaf(y, l, -b);          // y*l = b + b_lo exactly
   const float hi = a + b, bb = hi - a;
   const float lo = ((a - (hi - bb)) + (b - bb)) + (a_lo + b_lo);   // TwoSum error + the product tails
-  if (__builtin_expect(!(__builtin_fabsf(hi) < 126.0f), 0)) return cl_powf_cold(x, y);
-  const float k = __builtin_rintf(hi);
-  const float f = (hi - k) + lo;
-  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)k);
+  const float hc = __builtin_fminf(__builtin_fmaxf(hi, -160.0f), 160.0f);   // ldexp over/underflows from here
+  const float k = __builtin_rintf(hc);
+  const float f = (hc - k) + (hc == hi ? lo : 0.0f);
+  const float r = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)k);
+  // x == 0: log2 is -inf; pow(0, y) = 0 for y > 0, +inf for y < 0 (CLOUDSC: bases >= 0); NaN in, NaN out
+  if (x != x || y != y) return x + y;
+  return x == 0.0f ? (y > 0.0f ? 0.0f : __builtin_inff()) : r;
 }
 
 template <typename real>

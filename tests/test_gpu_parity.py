@@ -757,3 +757,30 @@ def test_fp32_fast_libm_ulp(lib):
     print("expf fast vs glibc: max %d ulp, %.1f %% equal; powf: max %d ulp, %.1f %% equal" % (
         d_exp.max(), 100.0 * np.mean(d_exp == 0), d_pow.max(), 100.0 * np.mean(d_pow == 0)))
     assert d_exp.max() <= 2 and d_pow.max() <= 2
+
+
+def test_fp32_fast_libm_special_values(lib):
+    """The float-internal expf / powf have no out-of-line fallback: their
+    special cases are branch-free and must still give expf's and powf's
+    answers -- overflow to +inf, underflow to 0, NaN in NaN out, pow of a zero
+    base 0 (y > 0) or +inf (y < 0) -- and agree with the glibc forms at the
+    edges of the range."""
+    inf, nan = np.float32(np.inf), np.float32(np.nan)
+    x = np.array([0.0, 1.0, -1.0, 88.0, 88.7, 89.0, 100.0, 1e30, inf, -87.0, -100.0, -104.0, -200.0, -inf, nan],
+                 np.float32)
+    px = np.array([0.0, 0.0, 1.0, 2.0, 1e-30, 1e30, inf, inf, 1e-38, nan, 2.0, 0.5], np.float32)
+    py = np.array([0.5, -0.5, 3.0, 0.5, 0.666, 1.5, 0.5, -0.5, 0.4, 0.5, nan, 200.0], np.float32)
+    out = {}
+    for which, (a, b) in {0: (x, x), 2: (x, x), 1: (px, py), 3: (px, py)}.items():
+        o = np.empty(a.size, np.float32)
+        ca.check(lib.cloudsc_debug_fp32_libm(0, which, a.ctypes.data, b.ctypes.data, o.ctypes.data, a.size))
+        out[which] = o
+    with np.errstate(over="ignore", under="ignore", invalid="ignore", divide="ignore"):
+        want_e = np.exp(x.astype(np.float64)).astype(np.float32)
+        want_p = np.power(px.astype(np.float64), py.astype(np.float64)).astype(np.float32)
+    for fast, ref, want in ((out[0], out[2], want_e), (out[1], out[3], want_p)):
+        fin = np.isfinite(want) & (want != 0)
+        # special values exactly; finite results within 2 ulp of the glibc forms
+        assert np.array_equal(np.isnan(fast), np.isnan(want)), (fast, want)
+        assert np.array_equal(fast[~fin & ~np.isnan(want)], want[~fin & ~np.isnan(want)]), (fast, want)
+        assert ulp_distance(fast[fin], ref[fin]).max() <= 2, (fast[fin], ref[fin])
