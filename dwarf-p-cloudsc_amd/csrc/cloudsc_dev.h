@@ -522,14 +522,29 @@ CLOUDSC_HD real cl_div_p(const P&, typename std::common_type<real>::type n, cons
 #endif
   return cl_div(static_cast<real>(n), rd);
 }
-// a known divisor with its RN(1/d): the FAST form is the same single
-// correction, the exact one cl_div's two (the IEEE quotient)
+// a known divisor with its RN(1/d): the FAST form is one multiply by it (within
+// 1.5 ulp), the exact one cl_div's correction steps (the IEEE quotient); the
+// FAST square root is v_sqrt_f32 (1 ulp) instead of the correctly rounded
+// sequence (-0.6 % fp32, profiles/r03/experiment_fp32_sqrt_known_div_ab.txt)
 template <typename real, typename P>
 CLOUDSC_HD real cl_div_known_p(const P& c, typename std::common_type<real>::type n, real d, real rcp_d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) return n * rcp_d;
+#endif
   return cl_div_p<real>(c, n, Recip<real>{d, rcp_d});
 }
 template <typename real, typename P>
+CLOUDSC_HD real cl_sqrt_p(const P&, typename std::common_type<real>::type x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) return __builtin_amdgcn_sqrtf(x);
+#endif
+  return sqrt(x);
+}
+template <typename real, typename P>
 CLOUDSC_HD real cl_div_lit_p(const P& c, typename std::common_type<real>::type n, real d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (LibmFast<P>::value) return n * (real(1) / d);
+#endif
   return cl_div_p<real>(c, n, Recip<real>{d, real(1) / d});
 }
 

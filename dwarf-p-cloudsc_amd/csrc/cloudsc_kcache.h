@@ -736,7 +736,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
         const real zcorr2 = cl_div_p<real>(c, (cl_pow<real>(c, cl_div_lit_p<real>(c, ztp1, R(273.0)), R(1.5)) * R(393.0)), (ztp1 + R(120.0)));
         const real zsubsat = fmax(zzrh * zqsliq - zqe, R(0.0));
         const real zbeta = ((((cl_div_p<real>(c, R(0.5), zqsliq)) * (ztp1 * ztp1)) * zesatliq) * c.rcl_const1r) * (cl_div_p<real>(c, zcorr2, zevap_denom)) *
-                           (cl_div_p<real>(c, R(0.78), cl_pow<real>(c, zlambda, c.rcl_const4r)) + cl_div_p<real>(c, (c.rcl_const2r * sqrt(zrho * zfallcorr)), (sqrt(zcorr2) * cl_pow<real>(c, zlambda, c.rcl_const3r))));
+                           (cl_div_p<real>(c, R(0.78), cl_pow<real>(c, zlambda, c.rcl_const4r)) + cl_div_p<real>(c, (c.rcl_const2r * cl_sqrt_p<real>(c, zrho * zfallcorr)), (cl_sqrt_p<real>(c, zcorr2) * cl_pow<real>(c, zlambda, c.rcl_const3r))));
         const real zdenom = R(1.0) + zbeta * c.ptsphy;
         const real zdpevap = cl_div_p<real>(c, (((zcovpclr * zbeta) * c.ptsphy) * zsubsat), zdenom);
         const real zevap = fmin(zdpevap, zqxfg[QR]);
@@ -753,7 +753,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       if (zqe < zzrh * zqsice) {
         const real x = cs.zcovptot * zdtgdp;
         const real zpreclr = cl_div_p<real>(c, (zqxfg[QS] * zcovpclr), copysign(fmax(fabs(x), zepsilon), x));
-        const real zbeta1 = cl_div_p<real>(c, ((cl_div_known_p<real>(c, sqrt(cl_div_p<real>(c, pap_k, cc.paph_sfc)), c.rvrfactor, c.rvrfactor_rcp)) * zpreclr), fmax(zcovpclr, zepsec));
+        const real zbeta1 = cl_div_p<real>(c, ((cl_div_known_p<real>(c, cl_sqrt_p<real>(c, cl_div_p<real>(c, pap_k, cc.paph_sfc)), c.rvrfactor, c.rvrfactor_rcp)) * zpreclr), fmax(zcovpclr, zepsec));
         const real zbeta = c.rg_rpecons * cl_pow<real>(c, zbeta1, R(0.5777));
         const real zdenom = R(1.0) + (zbeta * c.ptsphy) * zcorqsice;
         const real zdpr = ((cl_div_p<real>(c, ((zcovpclr * zbeta) * (zqsice - zqe)), zdenom)) * zdp) * c.zrg_r;
