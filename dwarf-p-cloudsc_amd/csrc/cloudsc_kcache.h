@@ -1072,6 +1072,17 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
     if (PFM) load_early<real>(nxt_e, A, u2, u3, lev0, klev, nproma, lo);
     if (PFA) load_level<real, AER>(nxt, A, u2, u3, lev0, klev, nproma, lo);
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // PF 1: drain the prologue's loads once (per segment) before the level loop.
+  // The level-(k+1) prefetch at the top of each level first copies the previous
+  // prefetch (cur = nxt); the waitcnt pass merges the loop header's two entries
+  // (prologue, latch) conservatively and then made EVERY level wait for part of
+  // the loads it had just issued -- a full memory round trip per level.  With
+  // the prologue drained, the header needs no vmcnt wait: fp32 KSEG -3.7 %
+  // (profiles/r03/experiment_prologue_drain_ab.txt).  (PF 3, the fp64 default,
+  // measured neutral and keeps its schedule.)
+  if constexpr (PFX) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt(7), lgkmcnt(15)
+#endif
 
   // fp32: the parameter block copied into VGPRs once per call (each value an
   // opaque per-lane copy), so the level loop reads every parameter from a
