@@ -271,3 +271,26 @@ def test_kseg_more_blocks_than_grid_y_limit(lib, ds):
     for a, b in zip(stats[2], stats[64]):
         assert a[:3] == b[:3]
         assert abs(a[3] - b[3]) <= 1e-12 * max(abs(b[3]), 1e-300) and abs(a[4] - b[4]) <= 1e-12 * abs(b[4])
+
+
+def test_state_field_placement_is_transparent(lib, ds):
+    """The diagnostic field placements of cloudsc_debug_set_state_layout (one
+    arena with staggered fields, and contiguous allocations) change where the
+    state's fields live in HBM, never what the kernels compute: every field
+    bit-equal to the default placement, for fp64 and fp32, and the knob
+    resets to the default."""
+    lib.cloudsc_debug_set_state_layout.argtypes = [C.c_longlong, C.c_uint]
+    for precision in (ca.FP64, ca.FP32):
+        out = {}
+        try:
+            for stagger, flags in ((-1, 0), (0, 0), (4608, 0), (-1, 4)):
+                ca.check(lib.cloudsc_debug_set_state_layout(stagger, flags))
+                g = ca.GpuState(ds, 3000, 64, precision)
+                try:
+                    out[(stagger, flags)] = outputs_of(g, ca.VARIANT_KSEG)
+                finally:
+                    g.close()
+        finally:
+            ca.check(lib.cloudsc_debug_set_state_layout(-1, 0))
+        for key, o in out.items():
+            assert bitwise_mismatches(o, out[(-1, 0)]) == {}, (precision, key)
