@@ -414,6 +414,7 @@ def gpu_lib(path: Optional[str] = None):
     return lib
 
 
+EINVAL = -1
 EHANDOFF = -7
 # option bit of a variant argument: fp32 exp/pow with the glibc algorithms (bit-identical to the fp32 restatement)
 FP32_EXACT_LIBM = 0x100

@@ -85,7 +85,13 @@ int param_set_upload(ParamSet* ps, int device, const cloudsc_params_t* p) {
   const DevParams<float> sp = fold_params<float>(*p);
   std::memcpy(blk.data(), &dp, sizeof(dp));
   std::memcpy(blk.data() + kSpOffset, &sp, sizeof(sp));
-  HIPCHK(hipMemcpy(ps->dev, blk.data(), kParamBlockBytes, hipMemcpyHostToDevice));
+  // hipMemcpy from pageable memory may return before the bytes have reached the
+  // device, and the launches that read them run on non-blocking streams, which
+  // do not wait for the null stream: a state created right after another one's
+  // destruction read part of a stale parameter block in its first launch.
+  // Copy on the null stream and wait for it.
+  HIPCHK(hipMemcpyAsync(ps->dev, blk.data(), kParamBlockBytes, hipMemcpyHostToDevice, nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));
   ps->device = device;
   ps->aer = p->laericesed || p->laericeauto;
   ps->ncldtop = p->ncldtop;
@@ -99,7 +105,8 @@ int param_set_copy(ParamSet* dst, const ParamSet* src) {
     hipError_t e = hipMalloc(&dst->dev, kParamBlockBytes);
     if (e != hipSuccess) { dst->dev = nullptr; hip_fail(e, "hipMalloc(params)"); return CLOUDSC_ENOMEM; }
   }
-  HIPCHK(hipMemcpy(dst->dev, src->dev, kParamBlockBytes, hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpyAsync(dst->dev, src->dev, kParamBlockBytes, hipMemcpyDeviceToDevice, nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));   // D2D hipMemcpy does not wait either (param_set_upload)
   dst->device = src->device;
   dst->aer = src->aer;
   dst->ncldtop = src->ncldtop;
@@ -589,7 +596,9 @@ int kseg_check(int device, void* stream, void* scratch) {
   HIPCHK(hipMemcpy(w, scratch, sizeof(w), hipMemcpyDeviceToHost));
   const unsigned err = w[2] == kKsegTag ? w[1] : 0u;   // no tag: no KSEG launch on this workspace yet
   if (err) {
-    HIPCHK(hipMemset((unsigned*)scratch + 1, 0, sizeof(unsigned)));
+    // on the launches' stream, and waited for: the next launch must not race it
+    HIPCHK(hipMemsetAsync((unsigned*)scratch + 1, 0, sizeof(unsigned), (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
     char msg[96];
     std::snprintf(msg, sizeof(msg), "KSEG: %u segment hand-offs timed out", err);
     set_error_text(msg);

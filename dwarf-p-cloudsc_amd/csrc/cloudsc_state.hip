@@ -136,12 +136,8 @@ void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
   return slots[id];
 }
 
-// diagnostic allocation flags of the state's fields (cloudsc_debug_set_state_layout)
-std::atomic<unsigned> g_alloc_flags{0};
-
 int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
-  const unsigned fl = g_alloc_flags.load();
-  hipError_t e = fl ? hipExtMallocWithFlags(p, bytes, fl) : hipMalloc(p, bytes);
+  hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
   s->allocs.push_back(*p);
   return CLOUDSC_OK;
@@ -287,8 +283,12 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
 }
 
 int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags) {
+  // alloc_flags (hipExtMallocWithFlags) are refused: once a state whose fields
+  // were hipDeviceMallocContiguous allocations had been destroyed, every state
+  // the process created afterwards computed wrong values, default placement and
+  // fp64 included (ROCm 7.2 on MI355X; profiles/r03/contiguous_alloc_hazard.txt)
+  if (alloc_flags != 0) return CLOUDSC_EINVAL;
   g_layout_stagger.store(stagger < 0 ? -1 : stagger);
-  g_alloc_flags.store(alloc_flags);
   return CLOUDSC_OK;
 }
 
@@ -399,7 +399,10 @@ int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* re
     void* const* slot = valid_slot(s, id, &kind);
     const int nlev = kind == 0 ? s->klev : kind == 1 ? s->klev + 1 : kind == 2 ? 5 * s->klev : 1;
     if (!ref->field[id]) { e = hipErrorInvalidValue; break; }
-    e = hipMemcpy(dref, ref->field[id], (size_t)nlev * ref->klon * sizeof(double), hipMemcpyHostToDevice);
+    // on the state's stream, ordered before the kernel that reads it (a null-stream
+    // hipMemcpy from pageable memory can still be in flight when it returns)
+    e = hipMemcpyAsync(dref, ref->field[id], (size_t)nlev * ref->klon * sizeof(double), hipMemcpyHostToDevice,
+                       s->stream);
     if (e != hipSuccess) break;
     if (s->precision == CLOUDSC_FP64)
       hipLaunchKernelGGL(stats_kernel<double>, dim3(s->nblocks), dim3(256), 0, s->stream, (const double*)*slot,

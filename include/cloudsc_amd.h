@@ -209,9 +209,11 @@ int cloudsc_debug_set_kseg_schedule(int nseg, int grid);
  * default): one device allocation per field.  >= 0: all fields of a state in
  * one allocation, field i starting at a 2 MiB boundary plus (i * stagger) mod
  * 2 MiB -- for measuring how the HBM placement of the ~47 concurrently
- * streamed fields affects the kernel time (tools/ab_layout.py).  alloc_flags:
- * 0 = hipMalloc, else hipExtMallocWithFlags with these flags (e.g. 4 =
- * hipDeviceMallocContiguous) for the state's field allocations. */
+ * streamed fields affects the kernel time (tools/ab_layout.py).  alloc_flags
+ * must be 0 (CLOUDSC_EINVAL otherwise): states created after a destroyed state
+ * whose fields were hipDeviceMallocContiguous allocations computed wrong values
+ * (profiles/r03/contiguous_alloc_hazard.txt), so the library allocates with
+ * hipMalloc only. */
 int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags);
 
 /* Diagnostic: the kernels' single-precision exp/pow on the device, element-wise

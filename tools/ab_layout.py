@@ -7,8 +7,9 @@ s >= 0 = one arena, field i at a 2 MiB boundary + (i*s) mod 2 MiB) it creates
 round (so clock drift hits every state alike), and reports per layout the
 median kernel time of each replica and over all of them.
 
-A layout is stagger[:alloc_flags] (alloc_flags for hipExtMallocWithFlags, e.g.
-4 = hipDeviceMallocContiguous).
+A layout is stagger[:alloc_flags]; the library now refuses alloc_flags != 0
+(profiles/r03/contiguous_alloc_hazard.txt), the form stays for the records of
+experiment_field_placement.txt.
 
 usage: ab_layout.py [--precision fp64] [--reps 2] [--rounds 40] layout [layout ...]"""
 import argparse
