@@ -74,6 +74,45 @@ CLOUDSC_HD T ldg1(const T* ubase, size_t uidx, unsigned lane_bytes) {
   return __builtin_nontemporal_load((const T*)((const char*)(ubase + uidx) + lane_bytes));
 }
 
+// The same accesses with the uniform address made opaque first (fp32): several
+// accesses of one field at different uniform indices (the species planes)
+// otherwise share one 64-bit VGPR pointer, base + lane offset, and each adds its
+// index to it with a VALU op; with the uniform pointer opaque, every access is
+// the saddr + voffset form.  fp32 only: its level loop is VALU-issue-bound.
+template <typename T>
+CLOUDSC_HD T ldg1_u(const T* ubase, size_t uidx, unsigned lane_bytes) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const T* p = ubase + uidx;
+  asm("" : "+s"(p));   // (the asm's output is a generic pointer: global address space restated below)
+  using GT = const __attribute__((address_space(1))) T;
+  return __builtin_nontemporal_load((GT*)((const __attribute__((address_space(1))) char*)p + lane_bytes));
+#else
+  return ldg1(ubase, uidx, lane_bytes);
+#endif
+}
+template <typename T>
+CLOUDSC_HD void stg_u(T* ubase, size_t uidx, unsigned lane_bytes, typename std::common_type<T>::type v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  T* p = ubase + uidx;
+  asm("" : "+s"(p));
+  using GT = __attribute__((address_space(1))) T;
+  __builtin_nontemporal_store(v, (GT*)((__attribute__((address_space(1))) char*)p + lane_bytes));
+#else
+  stg(ubase, uidx, lane_bytes, v);
+#endif
+}
+// species planes: the opaque-pointer form in fp32, the plain one in fp64
+template <typename T>
+CLOUDSC_HD T ldg1_sp(const T* ubase, size_t uidx, unsigned lane_bytes) {
+  if constexpr (sizeof(T) == 4) return ldg1_u(ubase, uidx, lane_bytes);
+  else return ldg1(ubase, uidx, lane_bytes);
+}
+template <typename T>
+CLOUDSC_HD void stg_sp(T* ubase, size_t uidx, unsigned lane_bytes, typename std::common_type<T>::type v) {
+  if constexpr (sizeof(T) == 4) stg_u(ubase, uidx, lane_bytes, v);
+  else stg(ubase, uidx, lane_bytes, v);
+}
+
 // Per-level inputs of one column (the prefetch unit).
 template <typename real>
 struct LevelIn {
@@ -99,8 +138,8 @@ CLOUDSC_HD void load_early(EarlyIn<real>& E, const KArgs<real>& A, size_t u2, si
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const size_t j = u3 + ((size_t)m * klev + k) * nproma;
-    E.pclv[m] = ldg1(A.pclv, j, lo);
-    E.ttcld[m] = ldg1(A.ttcld, j, lo);
+    E.pclv[m] = ldg1_sp(A.pclv, j, lo);
+    E.ttcld[m] = ldg1_sp(A.ttcld, j, lo);
   }
 }
 template <typename real, bool AER>
@@ -216,8 +255,8 @@ CLOUDSC_HD void load_level(LevelIn<real>& L, const KArgs<real>& A, size_t u2, si
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const size_t j = u3 + ((size_t)m * klev + k) * nproma;
-    L.pclv[m] = ldg1(A.pclv, j, lo);
-    L.ttcld[m] = ldg1(A.ttcld, j, lo);
+    L.pclv[m] = ldg1_sp(A.pclv, j, lo);
+    L.ttcld[m] = ldg1_sp(A.ttcld, j, lo);
   }
   L.phrsw = ldg1(A.phrsw, i, lo); L.phrlw = ldg1(A.phrlw, i, lo); L.pvervel = ldg1(A.pvervel, i, lo);
   L.psnde = ldg1(A.psnde, i, lo); L.psupsat = ldg1(A.psupsat, i, lo);
@@ -999,8 +1038,8 @@ CLOUDSC_HD void store_level(const KArgs<real>& A, size_t u2, size_t u3, int k, i
   stg(A.pcovptot, i, lo, po.zcovptot_out);
   stg(A.plude, i, lo, po.plude_k);   // INOUT: rewritten unchanged where not rescaled (no branch on a store)
 #pragma unroll
-  for (int m = 0; m < 4; m++) stg(A.tlcld, u3 + ((size_t)m * klev + k) * nproma, lo, po.ctend[m]);
-  stg(A.tlcld, u3 + ((size_t)4 * klev + k) * nproma, lo, R(0.0));
+  for (int m = 0; m < 4; m++) stg_sp(A.tlcld, u3 + ((size_t)m * klev + k) * nproma, lo, po.ctend[m]);
+  stg_sp(A.tlcld, u3 + ((size_t)4 * klev + k) * nproma, lo, R(0.0));
 }
 
 template <typename real, typename CS>
@@ -1174,8 +1213,9 @@ __device__ __forceinline__ void kcache_levels(cptr<KArgs<real>> ka, cptr<PT> cpa
     {
       const KArgs<real>& A = *(const KArgs<real>*)launder_uniform(ka);
       const auto& c = params_here<PVR>(pv, cpar);
-      store_level(A, u2, u3, k, klev, nproma, lo, physics, ls, po);
-      flux_level(c, A, uh + (size_t)(k + 1) * nproma, lo, cur, ls, po, nb.paph_k, nb.paph_n, cs);
+      const unsigned los = PVR ? launder_vgpr(lo0) : lo;
+      store_level(A, u2, u3, k, klev, nproma, los, physics, ls, po);
+      flux_level(c, A, uh + (size_t)(k + 1) * nproma, los, cur, ls, po, nb.paph_k, nb.paph_n, cs);
     }
 
     // ---- rotate carried state ----
