@@ -310,3 +310,47 @@ def test_state_field_placement_is_transparent(lib, ds):
                         sorted(bad), sorted(set((cols // 64).tolist())),
                         (int(levs.min()), int(levs.max())) if levs.size else None)
         assert diff == {}, (precision, diff)
+
+
+@pytest.mark.parametrize("precision", [ca.FP64, ca.FP32])
+def test_kseg_shared_workspace_alternating_states(lib, ds, precision):
+    """Two states with different inputs (B = the template's columns rotated by
+    half, so every block carries other values between its segments) run
+    alternately through cloudsc_gpu_run on ONE caller-owned KSEG workspace.
+    Each launch finds the other state's carried values in the hand-off slots:
+    a consumer that read its slot before the producer's values were visible
+    would differ.  Every launch bit-equal to that state's own state-API run
+    (tools/handoff_stress.py is the long form)."""
+    ngptot, nproma = 3000, 64
+    ds_b = ds.copy()
+    for k, v in ds_b.inputs.items():
+        if v.ndim >= 1 and v.shape[-1] == ds.klon:
+            ds_b.inputs[k] = np.ascontiguousarray(np.roll(v, ds.klon // 2, axis=-1))
+    states = [ca.GpuState(d, ngptot, nproma, precision) for d in (ds, ds_b)]
+    hip = C.CDLL("libamdhip64.so.7")
+    ws = C.c_void_p()
+    try:
+        refs = [outputs_of(g, ca.VARIANT_KSEG) for g in states]
+        assert bitwise_mismatches(refs[0], refs[1]) != {}
+        fields = []
+        for g in states:
+            f = ca.Fields()
+            ca.check(lib.cloudsc_state_fields(g.h, C.byref(f)))
+            fields.append(f)
+        p = ca.Params.from_dict(ds.params)
+        ca.check(lib.cloudsc_gpu_init(0, C.byref(p)))
+        nbytes = lib.cloudsc_gpu_scratch_bytes(precision, ca.VARIANT_KSEG, ngptot, nproma, ds.klev)
+        assert hip.hipMalloc(C.byref(ws), C.c_size_t(nbytes)) == 0
+        for it in range(6):
+            i = it & 1
+            ca.check(lib.cloudsc_state_reset(states[i].h))     # plude from the pristine copy
+            ca.check(lib.cloudsc_state_sync(states[i].h))
+            ca.check(lib.cloudsc_gpu_run(0, None, precision, ca.VARIANT_KSEG, ngptot, nproma, ds.klev,
+                                         C.byref(fields[i]), ws))
+            ca.check(lib.cloudsc_gpu_check(0, None, ca.VARIANT_KSEG, ws))
+            assert bitwise_mismatches(states[i].outputs(), refs[i]) == {}, (it, i)
+    finally:
+        if ws.value:
+            hip.hipFree(ws)
+        for g in states:
+            g.close()
