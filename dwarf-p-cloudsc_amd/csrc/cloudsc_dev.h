@@ -299,13 +299,16 @@ inline float cl_exp_host(float x) { return cloudsc_libm::expf_split(x, cloudsc_l
 // above with CLOUDSC_FP32_EXACT_LIBM).  expf: x*log2(e) as an exact
 // head + tail (Cody-Waite with an fma), the hardware 2^f (v_exp_f32, 1 ulp on
 // |f| <= 1/2) and ldexp.  powf: log2 of the mantissa in [1/2, 1) by the
-// hardware log2 (v_log_f32) plus the exponent, y*log2(x) as a float-float
-// (products split with fma, TwoSum), then the same exp2 + ldexp.  Every
+// hardware log2 (v_log_f32) plus the exponent as a float-float (Fast2Sum),
+// y*log2(x) as a float-float (one product split with fma), then the same
+// exp2 + ldexp (about 20 operations, was 30 with a full TwoSum of two split
+// products; same accuracy, -0.3 % fp32 KSEG: the pow sites sit in branches most
+// waves skip, profiles/r03/experiment_fp32_powf_fast2sum_ab.txt).  Every
 // operation is float (2-cycle issue on gfx950, against 4 for the double
 // internals of glibc's forms).  No out-of-line calls: the special cases are
 // branch-free (expf: the argument clamped to [-104, 89], where ldexp over- and
 // underflows to +inf / 0 as expf does, NaN passed through; powf: the exponent
-// clamped likewise, a zero base gives 0 or +inf) -- a call site in the level
+// clamped likewise, a zero or infinite base gives 0 or +inf) -- a call site in the level
 // loop costs the register allocation 5 % of the fp32 kernel time even when it
 // is never taken (profiles/r03/experiment_fp32_nocold_ab.txt).  Accuracy:
 // tests/test_gpu_parity.py (test_fp32_fast_libm_ulp) measures <= 2 ulp against
@@ -326,17 +329,14 @@ __device__ __forceinline__ float cl_powf_fast(float x, float y) {
   const float m = __builtin_amdgcn_frexp_mantf(x);                 // x = m * 2^E, m in [1/2, 1)
   const float E = (float)__builtin_amdgcn_frexp_expf(x);
   const float l = __builtin_amdgcn_logf(m);                         // log2(m), in [-1, 0)
-  const float a = y * E, a_lo = __builtin_fmaf(y, E, -a);          // y*E = a + a_lo exactly
-  const float b = y * l, b_lo = __builtin_fmaf(y, l, -b);          // y*l = b + b_lo exactly
-  const float hi = a + b, bb = hi - a;
-  const float lo = ((a - (hi - bb)) + (b - bb)) + (a_lo + b_lo);   // TwoSum error + the product tails
-  const float hc = __builtin_fminf(__builtin_fmaxf(hi, -160.0f), 160.0f);   // ldexp over/underflows from here
-  const float k = __builtin_rintf(hc);
-  const float f = (hc - k) + (hc == hi ? lo : 0.0f);
-  const float r = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)k);
-  // x == 0: log2 is -inf; pow(0, y) = 0 for y > 0, +inf for y < 0 (CLOUDSC: bases >= 0); NaN in, NaN out
-  if (x != x || y != y) return x + y;
-  return x == 0.0f ? (y > 0.0f ? 0.0f : __builtin_inff()) : r;
+  const float t = E + l, t_lo = l - (t - E);                        // Fast2Sum (|E| >= |l| or E == 0): E + l = t + t_lo
+  const float p = y * t;
+  const float p_lo = __builtin_fmaf(y, t_lo, __builtin_fmaf(y, t, -p));   // y*(t + t_lo) = p + p_lo (+ O(2^-48 p))
+  // k clamped (NaN -> -256): ldexp over- and underflows from there, and the conversion is always defined
+  const float k = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(p), -256.0f), 256.0f);
+  const float r = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f((p - k) + p_lo), (int)k);
+  // x == 0 (log2 -inf) or +inf: p = +-inf, pow is +inf or 0 (CLOUDSC: bases >= 0); NaN in, NaN out through r
+  return __builtin_isinf(p) ? (p > 0.0f ? __builtin_inff() : 0.0f) : r;
 }
 
 template <typename real>
