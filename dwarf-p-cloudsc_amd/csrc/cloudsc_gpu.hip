@@ -300,18 +300,26 @@ size_t kseg_scratch_bytes(int nblocks, int nproma) {
 // kseg_bounds_sweep_*.jsonl), for one-wave items (2048 slots): 2 segments, the
 // second one smaller ("guided": the items dequeued last are short, so the tail
 // is short; lower levels also cost more per level) -- the split at NCLDTOP +
-// 60 % of the physics levels (re-tuned with the streaming I/O: 1.768 ms against
-// 1.788 at 62 %, profiles/r01/kseg_bounds_sweep_nt.jsonl); each hand-off costs 19 values out and in plus an
-// L1 invalidate, so fewer segments win once the tail is short.
+// a share of the physics levels: 60 % in rounds 1-2 (1.768 ms against 1.788 at
+// 62 %, profiles/r01/kseg_bounds_sweep_nt.jsonl); re-tuned in round 3 for the
+// current kernels, interleaved on three boxes (profiles/r03/kseg_split_sweep.txt):
+// fp32 50 % (-2.5 / -2.6 / -1.0 % against 60); fp64 stays at 60 % (55 %: -1.9 /
+// -0.8 / +0.8 %, within the box-to-box spread).  Each hand-off
+// costs 19 values out and in plus an L1 invalidate, so fewer segments win once
+// the tail is short.
 constexpr int kKsegNseg = 2;
-constexpr int kKsegSplitPct = 60;
+#ifdef CLOUDSC_KSEG_SPLIT_PCT   // experiment builds override both (make variant VFLAGS=-DCLOUDSC_KSEG_SPLIT_PCT=..)
+template <typename real> constexpr int kKsegSplitPct = CLOUDSC_KSEG_SPLIT_PCT;
+#else
+template <typename real> constexpr int kKsegSplitPct = sizeof(real) == 8 ? 60 : 50;
+#endif
 
-void kseg_bounds(int nseg, int klev, int ncldtop, int* lev) {
+void kseg_bounds(int nseg, int klev, int ncldtop, int split_pct, int* lev) {
   const int top = ncldtop - 1 < klev ? (ncldtop - 1 > 0 ? ncldtop - 1 : 0) : klev;
   const int phys = klev - top;
   lev[0] = 0;
   if (nseg == 2) {
-    lev[1] = top + (int)(((long long)kKsegSplitPct * phys + 50) / 100);
+    lev[1] = top + (int)(((long long)split_pct * phys + 50) / 100);
     if (lev[1] <= 0) lev[1] = 1;
     if (lev[1] >= klev) lev[1] = klev - 1;
   } else {
@@ -442,7 +450,7 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
     if (pa.nseg > klev) pa.nseg = klev;
     pa.nblocks = nblocks;
     for (int q = 0; q <= kMaxSeg; q++) pa.lev[q] = klev;
-    kseg_bounds(pa.nseg, klev, ps.ncldtop, pa.lev);
+    kseg_bounds(pa.nseg, klev, ps.ncldtop, kKsegSplitPct<real>, pa.lev);
 #ifdef CLOUDSC_DEBUG_KNOBS
     if (const char* e = getenv("CLOUDSC_KSEG_BOUNDS")) {   // explicit interior boundaries
       int n = 1, v = 0;
