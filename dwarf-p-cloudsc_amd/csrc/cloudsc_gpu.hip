@@ -303,15 +303,15 @@ size_t kseg_scratch_bytes(int nblocks, int nproma) {
 // a share of the physics levels: 60 % in rounds 1-2 (1.768 ms against 1.788 at
 // 62 %, profiles/r01/kseg_bounds_sweep_nt.jsonl); re-tuned in round 3 for the
 // current kernels, interleaved on three boxes (profiles/r03/kseg_split_sweep.txt):
-// fp32 50 % (-2.5 / -2.6 / -1.0 % against 60); fp64 stays at 60 % (55 %: -1.9 /
-// -0.8 / +0.8 %, within the box-to-box spread).  Each hand-off
+// fp32 50 % (-2.5 / -2.6 / -1.0 % against 60), fp64 55 % (-1.9 / -0.8 / +0.8 /
+// -1.6 % on four boxes); 3 or 4 guided segments are 2.6-12 % slower.  Each hand-off
 // costs 19 values out and in plus an L1 invalidate, so fewer segments win once
 // the tail is short.
 constexpr int kKsegNseg = 2;
 #ifdef CLOUDSC_KSEG_SPLIT_PCT   // experiment builds override both (make variant VFLAGS=-DCLOUDSC_KSEG_SPLIT_PCT=..)
 template <typename real> constexpr int kKsegSplitPct = CLOUDSC_KSEG_SPLIT_PCT;
 #else
-template <typename real> constexpr int kKsegSplitPct = sizeof(real) == 8 ? 60 : 50;
+template <typename real> constexpr int kKsegSplitPct = sizeof(real) == 8 ? 55 : 50;
 #endif
 
 void kseg_bounds(int nseg, int klev, int ncldtop, int split_pct, int* lev) {
