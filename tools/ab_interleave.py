@@ -100,8 +100,9 @@ def main():
     base = ms[0]
     for path, m in zip(a.libs, ms):
         ratio = stt.median(x / y for x, y in zip(m, base))
-        print("%-34s median %.4f ms  min %.4f ms  ratio-to-first %.4f" % (
-            os.path.basename(path), stt.median(m), min(m), ratio), flush=True)
+        q = stt.quantiles(m, n=10)
+        print("%-34s median %.4f ms  min %.4f ms  p10 %.4f  p90 %.4f  ratio-to-first %.4f" % (
+            os.path.basename(path), stt.median(m), min(m), q[0], q[-1], ratio), flush=True)
 
 
 if __name__ == "__main__":
