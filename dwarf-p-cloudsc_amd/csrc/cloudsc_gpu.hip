@@ -90,8 +90,14 @@ int param_set_upload(ParamSet* ps, int device, const cloudsc_params_t* p) {
   // do not wait for the null stream: a state created right after another one's
   // destruction read part of a stale parameter block in its first launch.
   // Copy on the null stream and wait for it.
+#ifdef CLOUDSC_DEBUG_UNORDERED_PARAM_UPLOAD
+  // diagnostic build only: the round-3 upload, unordered with the launches
+  // (profiles/r04/contiguous_alloc_hazard.txt re-introduces it on purpose)
+  HIPCHK(hipMemcpy(ps->dev, blk.data(), kParamBlockBytes, hipMemcpyHostToDevice));
+#else
   HIPCHK(hipMemcpyAsync(ps->dev, blk.data(), kParamBlockBytes, hipMemcpyHostToDevice, nullptr));
   HIPCHK(hipStreamSynchronize(nullptr));
+#endif
   ps->device = device;
   ps->aer = p->laericesed || p->laericeauto;
   ps->ncldtop = p->ncldtop;

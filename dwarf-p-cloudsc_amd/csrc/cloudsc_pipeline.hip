@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include <unistd.h>
@@ -306,3 +307,138 @@ int cloudsc_debug_host_pinned(const void* ptr, long long bytes) {
 
 }  // extern "C"
 
+// ---------------------------------------------------------------------------
+// C ABI: one synchronous step on host arrays from any host thread
+// (cloudsc_host_run).  This is what a per-block caller such as the reference
+// C dwarf's OpenMP loop needs (cloudsc_driver.c:183-217 calls cloudsc_c() on
+// one NPROMA block at a time, from every thread): no creation call, no pinned
+// registration of the caller's arrays.  Each calling thread owns a context per
+// device -- its stream, device buffers sized for the largest call so far, a
+// KSEG workspace and a private parameter set, re-uploaded only when the
+// parameters change -- so concurrent callers never share state or race on a
+// parameter block.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct HostRunCtx {
+  hipStream_t st = nullptr;
+  void* buf[kNumFields] = {};
+  size_t cap[kNumFields] = {};
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  ParamSet params;
+  cloudsc_params_t cur{};
+  bool have_params = false;
+};
+// Device memory is not released at thread exit (the runtime may be gone by
+// then); cloudsc_host_run_release frees the calling thread's contexts.
+thread_local HostRunCtx* t_host_ctx[kMaxDevices] = {};
+
+int grow(void** p, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return CLOUDSC_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) { *p = nullptr; hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
+  *cap = bytes;
+  return CLOUDSC_OK;
+}
+
+// Copy the lanes of a field the kernel touches: the full blocks before the
+// last one as one run, then the last block's `bsize` active lanes of each of
+// its rows (a 2-D copy), so that lanes >= ngptot of the caller's arrays are
+// never read or written -- and a caller whose arrays start at column kidia-1
+// of a klon-wide block (cloudsc_c_dropin.c) is never read or written past the
+// end of its arrays.
+hipError_t copy_active(void* dst, const void* src, int kind, size_t eb, int nblocks, int nproma, int klev, int bsize,
+                       hipMemcpyKind dir, hipStream_t st) {
+  const size_t per = per_block_elems(kind, nproma, klev) * eb;
+  const size_t full = (size_t)(nblocks - 1) * per;
+  if (full) {
+    const hipError_t e = hipMemcpyAsync(dst, src, full, dir, st);
+    if (e != hipSuccess) return e;
+  }
+  const size_t rows = per / ((size_t)nproma * eb);
+  return hipMemcpy2DAsync((char*)dst + full, (size_t)nproma * eb, (const char*)src + full, (size_t)nproma * eb,
+                          (size_t)bsize * eb, rows, dir, st);
+}
+
+}  // namespace
+
+extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngptot, int nproma, int klev,
+                                const cloudsc_params_t* params, const cloudsc_fields_t* host) {
+  int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
+  if (rc) return rc;
+  if (!params || !host || !fields_complete(host)) return CLOUDSC_EINVAL;
+  if ((rc = check_params(params))) return rc;
+  const bool aer = params->laericesed || params->laericeauto;
+  if (aer && (!host->pre_ice || !host->picrit_aer || !host->pnice)) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(device));
+  HostRunCtx*& ctx = t_host_ctx[device];
+  if (!ctx) {
+    ctx = new HostRunCtx();
+    if (hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) {
+      delete ctx;
+      ctx = nullptr;
+      return CLOUDSC_EHIP;
+    }
+  }
+  if (!ctx->have_params || std::memcmp(&ctx->cur, params, sizeof(*params)) != 0) {
+    if ((rc = param_set_upload(&ctx->params, device, params))) return rc;
+    ctx->cur = *params;
+    ctx->have_params = true;
+  }
+  const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  const int bsize = ngptot - (nblocks - 1) * nproma;   // active lanes of the last block
+  const size_t es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
+  const void* const* hf = (const void* const*)host;
+  cloudsc_fields_t dev{};
+  void** df = (void**)&dev;
+  for (int i = 0; i < kNumFields; i++) {
+    if (!hf[i]) continue;
+    const FieldDesc& d = kFieldTable[i];
+    const size_t bytes = (size_t)nblocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : es);
+    if ((rc = grow(&ctx->buf[i], &ctx->cap[i], bytes))) return rc;
+    df[i] = ctx->buf[i];
+    if (d.dir != FD_OUT)
+      HIPCHK(copy_active(df[i], hf[i], d.kind, d.is_int ? sizeof(int) : es, nblocks, nproma, klev, bsize,
+                         hipMemcpyHostToDevice, ctx->st));
+  }
+  const int vk = variant_kind(variant);
+  if (vk == CLOUDSC_VARIANT_SCC || vk == CLOUDSC_VARIANT_KSEG) {
+    const long long nb = cloudsc_gpu_scratch_bytes(precision, vk, ngptot, nproma, klev);
+    if (nb <= 0) return CLOUDSC_EINVAL;
+    if ((rc = grow(&ctx->scratch, &ctx->scratch_bytes, (size_t)nb))) return rc;
+  }
+  rc = gpu_run_impl(device, ctx->st, precision, variant, ngptot, nproma, klev, &dev, ctx->scratch, nullptr,
+                    &ctx->params);
+  if (rc) {
+    (void)hipStreamSynchronize(ctx->st);
+    return rc;
+  }
+  for (int i = 0; i < kNumFields; i++) {
+    const FieldDesc& d = kFieldTable[i];
+    if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
+    HIPCHK(copy_active((void*)hf[i], df[i], d.kind, es, nblocks, nproma, klev, bsize, hipMemcpyDeviceToHost,
+                       ctx->st));
+  }
+  HIPCHK(hipStreamSynchronize(ctx->st));
+  if (vk == CLOUDSC_VARIANT_KSEG) return kseg_check(device, ctx->st, ctx->scratch);
+  return CLOUDSC_OK;
+}
+
+extern "C" int cloudsc_host_run_release(void) {
+  for (int d = 0; d < kMaxDevices; d++) {
+    HostRunCtx* ctx = t_host_ctx[d];
+    if (!ctx) continue;
+    (void)hipSetDevice(d);
+    if (ctx->st) { (void)hipStreamSynchronize(ctx->st); (void)hipStreamDestroy(ctx->st); }
+    for (void* q : ctx->buf) if (q) (void)hipFree(q);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    param_set_free(&ctx->params);
+    delete ctx;
+    t_host_ctx[d] = nullptr;
+  }
+  return CLOUDSC_OK;
+}

@@ -136,8 +136,20 @@ void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
   return slots[id];
 }
 
+#ifdef CLOUDSC_DEBUG_KNOBS
+// diagnostic build only: allocation flags of the state's fields
+// (hipExtMallocWithFlags), to re-run the round-3 contiguous-allocation
+// reproducer (profiles/r04/contiguous_alloc_hazard.txt)
+std::atomic<unsigned> g_alloc_flags{0};
+#endif
+
 int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
+#ifdef CLOUDSC_DEBUG_KNOBS
+  const unsigned fl = g_alloc_flags.load();
+  hipError_t e = fl ? hipExtMallocWithFlags(p, bytes, fl) : hipMalloc(p, bytes);
+#else
   hipError_t e = hipMalloc(p, bytes);
+#endif
   if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
   s->allocs.push_back(*p);
   return CLOUDSC_OK;
@@ -287,7 +299,11 @@ int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags) {
   // were hipDeviceMallocContiguous allocations had been destroyed, every state
   // the process created afterwards computed wrong values, default placement and
   // fp64 included (ROCm 7.2 on MI355X; profiles/r03/contiguous_alloc_hazard.txt)
+#ifdef CLOUDSC_DEBUG_KNOBS
+  g_alloc_flags.store(alloc_flags);
+#else
   if (alloc_flags != 0) return CLOUDSC_EINVAL;
+#endif
   g_layout_stagger.store(stagger < 0 ? -1 : stagger);
   return CLOUDSC_OK;
 }

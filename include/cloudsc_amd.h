@@ -400,6 +400,27 @@ int cloudsc_debug_host_pipeline_mapping(const cloudsc_host_pipeline_t *pipe, int
  * it was destroyed). */
 int cloudsc_debug_host_pinned(const void *ptr, long long bytes);
 
+/* ------------------------------------------------------------------------ */
+/* One synchronous step on host arrays, callable from any host thread        */
+/* ------------------------------------------------------------------------ */
+/* The per-block call of the reference C dwarf's OpenMP loop
+ * (src/cloudsc_c/cloudsc/cloudsc_driver.c:183-217 calls cloudsc_c() on one
+ * NPROMA block from every thread) moved to the device: copy the inputs and
+ * plude in (pageable memory is fine), run `variant`, copy the outputs and plude
+ * back, wait.  `host` holds HOST pointers in block layout, like
+ * cloudsc_cpu_run.  No cloudsc_gpu_init is needed: each calling thread keeps,
+ * per device, its own stream, device buffers (grown to the largest call), KSEG
+ * workspace and parameter set (uploaded again only when *params changes), so
+ * concurrent callers share nothing.  Same output contract as cloudsc_gpu_run.
+ * The drop-in cloudsc_c() of libcloudsc_c_amd_gpu.so (csrc/cloudsc_c_dropin.c)
+ * is built on it. */
+int cloudsc_host_run(int device, int precision, int variant, int ngptot, int nproma, int klev,
+                     const cloudsc_params_t *params, const cloudsc_fields_t *host);
+
+/* Free the calling thread's cloudsc_host_run contexts (device buffers, stream,
+ * parameter sets) on every device; the next cloudsc_host_run creates them again. */
+int cloudsc_host_run_release(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,15 @@ static void set_globals(const cloudsc_params_t *p, struct TECLDP *y)
   nclv = 5; ncldql = 1; ncldqi = 2; ncldqr = 3; ncldqs = 4; ncldqv = 5;
 }
 
+/* The parameter-module globals alone, for callers of cloudsc_c() itself
+ * (tests/test_dropin.py calls the reference kernel and the drop-in on one block). */
+void cloudsc_ref_set_params(const cloudsc_params_t *p)
+{
+  static struct TECLDP tecldp;
+  yrecldp = &tecldp;
+  set_globals(p, yrecldp);
+}
+
 /* fp64 only: the reference C kernel is hard-wired to double. */
 int cloudsc_ref_run(int nthreads, int ngptot, int nproma, int klev,
                     const cloudsc_params_t *p, const cloudsc_fields_t *f, double *seconds)
