@@ -36,8 +36,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)    # 0.2 s of kernels: a stable mean
     p.add_argument("--warmup", type=int, default=20,
-                   help="untimed steps; the board settles its shader clock over the first ~10-15 launches of the "
-                        "fp64 kernel (profiles/r02/clock_probe_bench_run.json)")
+                   help="minimum untimed steps; warm-up then continues by time until the per-launch kernel time "
+                        "is stable (the board settles its shader clock over the first ~10-15 launches of the fp64 "
+                        "kernel, profiles/r02/clock_probe_bench_run.json); the steps actually run are reported "
+                        "as prewarm_steps")
     p.add_argument("--ngptot", type=int, default=163840, help="columns per GPU")
     p.add_argument("--nproma", type=int, default=64,
                    help="NPROMA (block = workgroup); 64 is the measured best for the persistent kernel "
@@ -64,6 +66,22 @@ def parse():
     if a.variant is None:
         a.variant = "kseg"
     return a
+
+
+def prewarm_until_stable(g, variant, min_steps, np, batch=5, tol=0.005, floor=15, cap=400):
+    """Untimed launches until the kernel time is stable: batches of `batch`
+    launches, at least max(min_steps, floor) in all, until two consecutive batch
+    medians agree within `tol` (the shader clock has settled), at most `cap`.
+    Returns the number of launches run."""
+    n, prev = 0, None
+    need = max(min_steps, floor)
+    while n < cap:
+        m = float(np.median(g.run(variant, batch)))
+        n += batch
+        if n >= need and prev is not None and abs(m - prev) <= tol * prev:
+            break
+        prev = m
+    return n
 
 
 def cpu_baseline(ca, ds, nthreads):
@@ -179,9 +197,10 @@ def main():
     if not args.no_hbm_peak:          # every rank warms its own device the same way
         peak_meas = ca.hbm_copy_gbps(device, 4 << 30, 10)
 
-    if args.warmup > 0:
-        g.run(variant, args.warmup)
+    prewarm = prewarm_until_stable(g, variant, args.warmup, np)
     g.sync()
+    if kind == ca.VARIANT_KSEG:
+        g.kseg_clock(reset=True)                # the clock counters cover the timed launches only
     ctl.barrier()
     t0 = time.perf_counter()
     kernel_ms = g.run(variant, args.steps)      # one launch per step; its dispatch records its events
@@ -190,6 +209,16 @@ def main():
     ctl.barrier()
     wall = ctl.max(t1 - t0)
     k_avg_ms = ctl.max(float(np.mean(kernel_ms)))
+    sclk = g.kseg_clock() if kind == ca.VARIANT_KSEG else None
+    # every rank's own record, gathered to rank 0 (the reference's per-rank
+    # timing table, src/common/module/timer_mod.F90:160-167)
+    mine = {"rank": rank, "device": device, "local_rank": topo.local_rank, "ngptot": ncols,
+            "col_offset": col_offset, "wall_s": round(t1 - t0, 6),
+            "kernel_ms": round(float(np.mean(kernel_ms)), 4), "kernel_ms_min": round(float(np.min(kernel_ms)), 4),
+            "kernel_ms_median": round(float(np.median(kernel_ms)), 4),
+            "stream_gbs": round(peak_meas, 1) if peak_meas else None,
+            "sclk_ghz": round(sclk, 4) if sclk else None, "prewarm_steps": prewarm}
+    per_rank = ctl.gather_records(mine)
 
     # validation of the last step against reference.h5 (device-side statistics, combined over ranks)
     stats = ctl.gather_stats(g.validate())
@@ -232,8 +261,18 @@ def main():
                     else "float-internal expf/powf (hardware exp2/log2, exact argument reduction)",
             "ngptot_per_gpu": args.ngptot, "ngptot_total": total_cols, "klev": ds.klev,
             "nproma": args.nproma, "variant": args.variant, "parallelism": "columns sharded, %d GPU(s)" % world},
+        "prewarm_steps": prewarm,
         "kernel_ms": round(k_avg_ms, 4),
         "kernel_ms_min": round(float(np.min(kernel_ms)), 4),
+        "kernel_ms_median": round(float(np.median(kernel_ms)), 4),
+        "kernel_ms_p10": round(float(np.percentile(kernel_ms, 10)), 4),
+        "kernel_ms_p90": round(float(np.percentile(kernel_ms, 90)), 4),
+        "kernel_ms_method": "HIP events recorded by each launch's own dispatch on the state's stream; mean over "
+                            "ranks' means is the max over ranks",
+        "sclk_ghz": round(sclk, 4) if sclk else None,
+        "sclk_method": "effective shader clock of the timed launches: each workgroup's s_memtime cycles over its "
+                       "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",
+        "per_rank": per_rank,
         "validation_worst_rel_l1": worst,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -556,6 +556,13 @@ class GpuState:
     def sync(self) -> None:
         check(self.lib.cloudsc_state_sync(self.h))
 
+    def kseg_clock(self, reset: bool = False) -> float:
+        """Effective shader clock (GHz) of the KSEG launches since the last reset
+        (cloudsc_state_kseg_clock); 0.0 before any KSEG launch."""
+        ghz = C.c_double()
+        check(self.lib.cloudsc_state_kseg_clock(self.h, int(reset), C.byref(ghz)))
+        return ghz.value
+
     def reset(self) -> None:
         check(self.lib.cloudsc_state_reset(self.h))
 

@@ -91,6 +91,16 @@ class Control:
         self.dist.all_gather(parts, t)
         return combine_stats([p.tolist() for p in parts])
 
+    def gather_records(self, rec: dict) -> List[dict]:
+        """Every rank's record (a small JSON-able dict), in rank order, on every
+        rank -- the per-rank timing table the reference gathers to rank 0
+        (src/common/module/timer_mod.F90:160-167)."""
+        if self.dist is None:
+            return [dict(rec)]
+        out: List[dict] = [None] * self.topo.world   # type: ignore[list-item]
+        self.dist.all_gather_object(out, dict(rec))
+        return out
+
     def close(self) -> None:
         if self.dist is not None:
             self.dist.destroy_process_group()

@@ -343,17 +343,19 @@ std::atomic<int> g_kseg_nseg{0}, g_kseg_grid{0};
 
 // KSEG workspace words: [0] dequeue counter, [1] timed-out hand-offs (sticky:
 // accumulated over launches until cloudsc_gpu_check reads and clears it),
-// [2] a tag marking [1] as initialised, [64..] per-sub-block flags.  This
+// [2] a tag marking [1] as initialised, [32..35] two 64-bit clock sums
+// (PersistArgs::clk, accumulated like [1]), [64..] per-sub-block flags.  This
 // kernel zeroes the counter and the flags before every launch of the low-level
 // entry points, and before the first launch on a state's workspace (later
 // launches of the state continue the counter and the flag stamps, KsegEpoch);
 // the first launch on a workspace (tag absent) also zeroes the error word.
 constexpr unsigned kKsegTag = 0xC105D5C1u;
+constexpr size_t kKsegClkOffset = 128;   // bytes: words [32..35]
 __global__ void __launch_bounds__(256) kseg_prepare_kernel(unsigned* ws, int nflags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     ws[0] = 0u;
-    if (ws[2] != kKsegTag) { ws[1] = 0u; ws[2] = kKsegTag; }
+    if (ws[2] != kKsegTag) { ws[1] = 0u; ws[2] = kKsegTag; ws[32] = ws[33] = ws[34] = ws[35] = 0u; }
   }
   for (int j = i; j < nflags; j += gridDim.x * blockDim.x) ws[64 + j] = 0u;
 }
@@ -439,6 +441,7 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
     PersistArgs<real> pa;
     pa.counter = (unsigned*)scratch;
     pa.err = (unsigned*)scratch + 1;
+    pa.clk = (unsigned long long*)((char*)scratch + kKsegClkOffset);
     pa.flags = (unsigned*)((char*)scratch + 256);
     pa.state = (real*)((char*)scratch + kseg_ctl_bytes(nblocks, nproma));
     pa.nsub = kseg_nsub(nproma);
@@ -601,6 +604,22 @@ int gpu_run_impl(int device, void* stream, int precision, int variant, int ngpto
   return precision == CLOUDSC_FP64
              ? launch<double>(st, variant, exact_libm, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev)
              : launch<float>(st, variant, exact_libm, f, ngptot, nproma, klev, scratch, plude_in, *ps, ep, lev);
+}
+
+int kseg_clock(int device, void* stream, void* scratch, bool reset, double* ghz, double* seconds) {
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  unsigned long long w[2] = {0, 0};
+  HIPCHK(hipMemcpy(w, (char*)scratch + kKsegClkOffset, sizeof(w), hipMemcpyDeviceToHost));
+  int khz = 0;
+  HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+  if (ghz) *ghz = w[1] && khz > 0 ? (double)w[0] / (double)w[1] * (double)khz * 1e-6 : 0.0;
+  if (seconds) *seconds = khz > 0 ? (double)w[1] / ((double)khz * 1e3) : 0.0;
+  if (reset) {
+    HIPCHK(hipMemsetAsync((char*)scratch + kKsegClkOffset, 0, sizeof(w), (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  }
+  return CLOUDSC_OK;
 }
 
 int kseg_check(int device, void* stream, void* scratch) {

@@ -60,6 +60,11 @@ inline int variant_kind(int variant) { return variant & 0xff; }
 // waits for `stream` and returns CLOUDSC_EHANDOFF if the last KSEG launch on
 // `scratch` counted a timed-out segment hand-off
 int kseg_check(int device, void* stream, void* scratch);
+// waits for `stream`; the effective shader clock of the KSEG launches on
+// `scratch` since the last reset (sum of shader-clock cycles over sum of
+// real-time ticks of the workgroups, times the real-time rate) and the summed
+// workgroup-seconds behind it; reset zeroes the sums
+int kseg_clock(int device, void* stream, void* scratch, bool reset, double* ghz, double* seconds);
 
 }  // namespace cloudsc_impl
 

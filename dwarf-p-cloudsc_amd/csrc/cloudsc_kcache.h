@@ -1286,6 +1286,10 @@ struct PersistArgs {
   int nsub;               // 64-column sub-blocks per NPROMA block (one wave each)
   int sb_major;           // item order (segment, sub-block, block) instead of (segment, block, sub-block)
   unsigned spin_limit;    // polls before a consumer gives up (and counts an error)
+  // [0] += shader-clock cycles (s_memtime), [1] += 100 MHz real-time ticks
+  // (s_memrealtime) each workgroup spends in the kernel: their ratio is the
+  // effective shader clock of the launches (cloudsc_state_kseg_clock)
+  unsigned long long* clk;
   int lev[kMaxSeg + 1];
 };
 
@@ -1330,6 +1334,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
   // barriers no longer pair up across waves.
   const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;
   const unsigned one = threadIdx.x == 0 ? 1u : 0u;  // lane 0 counts, the others add 0
+  const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (wave0) {
       const unsigned old = __hip_atomic_fetch_add(P.counter, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1403,6 +1408,13 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       g_kseg_trace[4 * item + 3] = t_ready;
     }
 #endif
+  }
+  // the workgroup's time in the kernel, in shader cycles and real-time ticks
+  // (one vector atomic each, after the last item; no barrier follows)
+  const unsigned long long dclk = __builtin_amdgcn_s_memtime() - clk0, drt = __builtin_amdgcn_s_memrealtime() - rt0;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(P.clk, dclk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(P.clk + 1, drt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -313,17 +314,24 @@ int cloudsc_debug_host_pinned(const void* ptr, long long bytes) {
 // C dwarf's OpenMP loop needs (cloudsc_driver.c:183-217 calls cloudsc_c() on
 // one NPROMA block at a time, from every thread): no creation call, no pinned
 // registration of the caller's arrays.  Each calling thread owns a context per
-// device -- its stream, device buffers sized for the largest call so far, a
-// KSEG workspace and a private parameter set, re-uploaded only when the
-// parameters change -- so concurrent callers never share state or race on a
-// parameter block.
+// device -- its stream, a pinned staging buffer and a device buffer laid out
+// alike (grown to the largest call so far), a KSEG workspace and a private
+// parameter set, re-uploaded only when the parameters change -- so concurrent
+// callers never share state or race on a parameter block.
+//
+// Transfers: the active lanes of every input are packed on the host into the
+// staging buffer and go to the device in ONE copy; the outputs come back in one
+// copy and are unpacked.  Only lanes < ngptot of the caller's arrays are read
+// or written (a caller whose arrays start at column kidia-1 of a klon-wide
+// block, cloudsc_c_dropin.c, is never read or written past their end).
 // ---------------------------------------------------------------------------
 namespace {
 
 struct HostRunCtx {
   hipStream_t st = nullptr;
-  void* buf[kNumFields] = {};
-  size_t cap[kNumFields] = {};
+  char* stage = nullptr;    // pinned host
+  char* dbuf = nullptr;     // device, same layout
+  size_t cap = 0;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   ParamSet params;
@@ -334,34 +342,18 @@ struct HostRunCtx {
 // then); cloudsc_host_run_release frees the calling thread's contexts.
 thread_local HostRunCtx* t_host_ctx[kMaxDevices] = {};
 
-int grow(void** p, size_t* cap, size_t bytes) {
-  if (bytes <= *cap) return CLOUDSC_OK;
-  if (*p) (void)hipFree(*p);
-  *p = nullptr;
-  *cap = 0;
-  const hipError_t e = hipMalloc(p, bytes);
-  if (e != hipSuccess) { *p = nullptr; hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
-  *cap = bytes;
-  return CLOUDSC_OK;
-}
-
-// Copy the lanes of a field the kernel touches: the full blocks before the
-// last one as one run, then the last block's `bsize` active lanes of each of
-// its rows (a 2-D copy), so that lanes >= ngptot of the caller's arrays are
-// never read or written -- and a caller whose arrays start at column kidia-1
-// of a klon-wide block (cloudsc_c_dropin.c) is never read or written past the
-// end of its arrays.
-hipError_t copy_active(void* dst, const void* src, int kind, size_t eb, int nblocks, int nproma, int klev, int bsize,
-                       hipMemcpyKind dir, hipStream_t st) {
-  const size_t per = per_block_elems(kind, nproma, klev) * eb;
-  const size_t full = (size_t)(nblocks - 1) * per;
+// copy the active lanes between a caller's field and its packed image: the full
+// blocks before the last one as one run, then `bsize` lanes of each row of the
+// last block
+void pack_active(char* img, const char* fld, size_t per, size_t full, size_t row, size_t lanes, bool to_img) {
   if (full) {
-    const hipError_t e = hipMemcpyAsync(dst, src, full, dir, st);
-    if (e != hipSuccess) return e;
+    if (to_img) std::memcpy(img, fld, full);
+    else std::memcpy((char*)fld, img, full);
   }
-  const size_t rows = per / ((size_t)nproma * eb);
-  return hipMemcpy2DAsync((char*)dst + full, (size_t)nproma * eb, (const char*)src + full, (size_t)nproma * eb,
-                          (size_t)bsize * eb, rows, dir, st);
+  for (size_t off = full; off < full + per; off += row) {
+    if (to_img) std::memcpy(img + off, fld + off, lanes);
+    else std::memcpy((char*)fld + off, img + off, lanes);
+  }
 }
 
 }  // namespace
@@ -393,23 +385,58 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
   const int bsize = ngptot - (nblocks - 1) * nproma;   // active lanes of the last block
   const size_t es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
   const void* const* hf = (const void* const*)host;
+  // image layout: the inputs (and plude) first, then the outputs; 256-byte aligned fields
+  size_t off[kNumFields] = {}, bytes[kNumFields] = {};
+  size_t in_end = 0, total = 0;
+  for (int pass = 0; pass < 2; pass++)
+    for (int i = 0; i < kNumFields; i++) {
+      const FieldDesc& d = kFieldTable[i];
+      if (!hf[i] || (pass == 0) != (d.dir != FD_OUT)) continue;
+      bytes[i] = (size_t)nblocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : es);
+      off[i] = total;
+      total += (bytes[i] + 255) & ~(size_t)255;
+      if (pass == 0) in_end = total;
+    }
+  if (total > ctx->cap) {
+    if (ctx->stage) (void)hipHostFree(ctx->stage);
+    if (ctx->dbuf) (void)hipFree(ctx->dbuf);
+    ctx->stage = ctx->dbuf = nullptr;
+    ctx->cap = 0;
+    hipError_t e = hipHostMalloc((void**)&ctx->stage, total, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->dbuf, total);
+    if (e != hipSuccess) {
+      if (ctx->stage) (void)hipHostFree(ctx->stage);
+      ctx->stage = nullptr;
+      hip_fail(e, "host_run buffers");
+      return CLOUDSC_ENOMEM;
+    }
+    ctx->cap = total;
+  }
   cloudsc_fields_t dev{};
   void** df = (void**)&dev;
   for (int i = 0; i < kNumFields; i++) {
     if (!hf[i]) continue;
     const FieldDesc& d = kFieldTable[i];
-    const size_t bytes = (size_t)nblocks * per_block_elems(d.kind, nproma, klev) * (d.is_int ? sizeof(int) : es);
-    if ((rc = grow(&ctx->buf[i], &ctx->cap[i], bytes))) return rc;
-    df[i] = ctx->buf[i];
+    const size_t eb = d.is_int ? sizeof(int) : es;
+    const size_t per = per_block_elems(d.kind, nproma, klev) * eb;
+    df[i] = ctx->dbuf + off[i];
     if (d.dir != FD_OUT)
-      HIPCHK(copy_active(df[i], hf[i], d.kind, d.is_int ? sizeof(int) : es, nblocks, nproma, klev, bsize,
-                         hipMemcpyHostToDevice, ctx->st));
+      pack_active(ctx->stage + off[i], (const char*)hf[i], per, (size_t)(nblocks - 1) * per, (size_t)nproma * eb,
+                  (size_t)bsize * eb, true);
   }
+  HIPCHK(hipMemcpyAsync(ctx->dbuf, ctx->stage, in_end, hipMemcpyHostToDevice, ctx->st));
   const int vk = variant_kind(variant);
   if (vk == CLOUDSC_VARIANT_SCC || vk == CLOUDSC_VARIANT_KSEG) {
     const long long nb = cloudsc_gpu_scratch_bytes(precision, vk, ngptot, nproma, klev);
     if (nb <= 0) return CLOUDSC_EINVAL;
-    if ((rc = grow(&ctx->scratch, &ctx->scratch_bytes, (size_t)nb))) return rc;
+    if ((size_t)nb > ctx->scratch_bytes) {
+      if (ctx->scratch) (void)hipFree(ctx->scratch);
+      ctx->scratch = nullptr;
+      ctx->scratch_bytes = 0;
+      const hipError_t e = hipMalloc(&ctx->scratch, (size_t)nb);
+      if (e != hipSuccess) { ctx->scratch = nullptr; hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
+      ctx->scratch_bytes = (size_t)nb;
+    }
   }
   rc = gpu_run_impl(device, ctx->st, precision, variant, ngptot, nproma, klev, &dev, ctx->scratch, nullptr,
                     &ctx->params);
@@ -417,14 +444,19 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
     (void)hipStreamSynchronize(ctx->st);
     return rc;
   }
+  // plude (INOUT) sits in the input region: bring back from it to the end
+  const int iplude = (int)(offsetof(cloudsc_fields_t, plude) / sizeof(void*));
+  HIPCHK(hipMemcpyAsync(ctx->stage + off[iplude], ctx->dbuf + off[iplude], total - off[iplude],
+                        hipMemcpyDeviceToHost, ctx->st));
+  HIPCHK(hipStreamSynchronize(ctx->st));
+  if (vk == CLOUDSC_VARIANT_KSEG && (rc = kseg_check(device, ctx->st, ctx->scratch))) return rc;
   for (int i = 0; i < kNumFields; i++) {
     const FieldDesc& d = kFieldTable[i];
     if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
-    HIPCHK(copy_active((void*)hf[i], df[i], d.kind, es, nblocks, nproma, klev, bsize, hipMemcpyDeviceToHost,
-                       ctx->st));
+    const size_t per = per_block_elems(d.kind, nproma, klev) * es;
+    pack_active(ctx->stage + off[i], (const char*)hf[i], per, (size_t)(nblocks - 1) * per, (size_t)nproma * es,
+                (size_t)bsize * es, false);
   }
-  HIPCHK(hipStreamSynchronize(ctx->st));
-  if (vk == CLOUDSC_VARIANT_KSEG) return kseg_check(device, ctx->st, ctx->scratch);
   return CLOUDSC_OK;
 }
 
@@ -434,7 +466,8 @@ extern "C" int cloudsc_host_run_release(void) {
     if (!ctx) continue;
     (void)hipSetDevice(d);
     if (ctx->st) { (void)hipStreamSynchronize(ctx->st); (void)hipStreamDestroy(ctx->st); }
-    for (void* q : ctx->buf) if (q) (void)hipFree(q);
+    if (ctx->stage) (void)hipHostFree(ctx->stage);
+    if (ctx->dbuf) (void)hipFree(ctx->dbuf);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     param_set_free(&ctx->params);
     delete ctx;

@@ -136,20 +136,13 @@ void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
   return slots[id];
 }
 
-#ifdef CLOUDSC_DEBUG_KNOBS
-// diagnostic build only: allocation flags of the state's fields
-// (hipExtMallocWithFlags), to re-run the round-3 contiguous-allocation
-// reproducer (profiles/r04/contiguous_alloc_hazard.txt)
+// diagnostic allocation flags of the state's fields (cloudsc_debug_set_state_layout,
+// hipExtMallocWithFlags); 0 = hipMalloc
 std::atomic<unsigned> g_alloc_flags{0};
-#endif
 
 int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
-#ifdef CLOUDSC_DEBUG_KNOBS
   const unsigned fl = g_alloc_flags.load();
   hipError_t e = fl ? hipExtMallocWithFlags(p, bytes, fl) : hipMalloc(p, bytes);
-#else
-  hipError_t e = hipMalloc(p, bytes);
-#endif
   if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
   s->allocs.push_back(*p);
   return CLOUDSC_OK;
@@ -169,6 +162,7 @@ struct Arena {
 size_t arena_span(size_t bytes) { return (bytes + kArenaAlign - 1) / kArenaAlign * kArenaAlign + kArenaAlign; }
 int field_alloc(cloudsc_gpu_state* s, Arena& ar, void** p, size_t bytes) {
   if (!ar.base) return dalloc(s, p, bytes);
+  // stagger < 2 MiB (cloudsc_debug_set_state_layout) and n < 64: no overflow
   *p = ar.base + ar.off + (size_t)(((long long)ar.n * ar.stagger) % (long long)kArenaAlign);
   ar.off += arena_span(bytes);
   ar.n++;
@@ -295,16 +289,18 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
 }
 
 int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags) {
-  // alloc_flags (hipExtMallocWithFlags) are refused: once a state whose fields
-  // were hipDeviceMallocContiguous allocations had been destroyed, every state
-  // the process created afterwards computed wrong values, default placement and
-  // fp64 included (ROCm 7.2 on MI355X; profiles/r03/contiguous_alloc_hazard.txt)
-#ifdef CLOUDSC_DEBUG_KNOBS
+  // Round 3 refused alloc_flags after states created behind a destroyed
+  // hipDeviceMallocContiguous state computed wrong values.  The cause was the
+  // parameter upload (a null-stream hipMemcpy from pageable memory, unordered
+  // with the launches on the state's non-blocking stream, fixed in
+  // param_set_upload): with that upload re-introduced the failure reappears,
+  // in KCACHE as in KSEG, and with the ordered upload 44 of 44 runs of the same
+  // sequence are bit-exact to the oracle (profiles/r04/contiguous_alloc_hazard.txt).
+  // A stagger must keep every field aligned for the widest element (a multiple
+  // of 256 bytes) and is taken modulo the 2 MiB arena alignment.
+  if (stagger >= 0 && stagger % 256 != 0) return CLOUDSC_EINVAL;
   g_alloc_flags.store(alloc_flags);
-#else
-  if (alloc_flags != 0) return CLOUDSC_EINVAL;
-#endif
-  g_layout_stagger.store(stagger < 0 ? -1 : stagger);
+  g_layout_stagger.store(stagger < 0 ? -1 : stagger % (long long)kArenaAlign);
   return CLOUDSC_OK;
 }
 
@@ -334,6 +330,7 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
       if (nb <= 0) return CLOUDSC_EINVAL;
       int rc0 = dalloc(s, &ws, (size_t)nb);
       if (rc0) return rc0;
+      HIPCHK(hipMemsetAsync(ws, 0, 256, s->stream));   // control words (the first launch zeroes the rest)
     }
     scratch = ws;
   }
@@ -367,6 +364,15 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
   }
   if (rc != CLOUDSC_OK) s->kseg_epoch.ready = false;   // zero the workspace again before the next launch
   return rc;
+}
+
+int cloudsc_state_kseg_clock(cloudsc_gpu_state_t* s, int reset, double* ghz) {
+  if (!s || !ghz) return CLOUDSC_EINVAL;
+  *ghz = 0.0;
+  if (!s->kseg_ws) {   // no KSEG launch yet: nothing measured; a reset is a no-op
+    return CLOUDSC_OK;
+  }
+  return kseg_clock(s->device, s->stream, s->kseg_ws, reset != 0, ghz, nullptr);
 }
 
 int cloudsc_state_sync(cloudsc_gpu_state_t* s) {

@@ -209,11 +209,13 @@ int cloudsc_debug_set_kseg_schedule(int nseg, int grid);
  * default): one device allocation per field.  >= 0: all fields of a state in
  * one allocation, field i starting at a 2 MiB boundary plus (i * stagger) mod
  * 2 MiB -- for measuring how the HBM placement of the ~47 concurrently
- * streamed fields affects the kernel time (tools/ab_layout.py).  alloc_flags
- * must be 0 (CLOUDSC_EINVAL otherwise): states created after a destroyed state
- * whose fields were hipDeviceMallocContiguous allocations computed wrong values
- * (profiles/r03/contiguous_alloc_hazard.txt), so the library allocates with
- * hipMalloc only. */
+ * streamed fields affects the kernel time (tools/ab_layout.py).  stagger must
+ * be a multiple of 256 bytes (CLOUDSC_EINVAL otherwise) and is taken modulo
+ * 2 MiB.  alloc_flags != 0: the state's allocations are made with
+ * hipExtMallocWithFlags(alloc_flags) (e.g. 4 = hipDeviceMallocContiguous).
+ * (Round 3 refused the flags after wrong values in states created behind a
+ * destroyed contiguous state; the cause was an unordered parameter upload,
+ * fixed: profiles/r04/contiguous_alloc_hazard.txt.) */
 int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags);
 
 /* Diagnostic: the kernels' single-precision exp/pow on the device, element-wise
@@ -347,6 +349,15 @@ int cloudsc_state_run(cloudsc_gpu_state_t *state, int variant, int reps, float *
 
 /* Wait for all work of the state's stream. */
 int cloudsc_state_sync(cloudsc_gpu_state_t *state);
+
+/* Measurement: the effective shader clock of the state's KSEG launches since
+ * the last reset, in GHz -- every workgroup adds the shader-clock cycles
+ * (s_memtime) and the 100 MHz real-time ticks (s_memrealtime) it spent in the
+ * kernel to two counters in the KSEG workspace; *ghz = cycles / ticks x the
+ * real-time rate (0 before any KSEG launch).  Waits for the state's stream;
+ * reset != 0 zeroes the counters afterwards.  bench.py reports it beside the
+ * kernel time (the fp64 kernel follows the board's clock). */
+int cloudsc_state_kseg_clock(cloudsc_gpu_state_t *state, int reset, double *ghz);
 
 /* Field-wise statistics vs a KLON-column reference, computed on the device
  * (modulo indexing; no expanded reference in host or device memory). */

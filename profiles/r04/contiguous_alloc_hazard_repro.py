@@ -28,7 +28,7 @@ import oracle  # noqa: E402
 NG, NP = 3000, 64
 lib = ca.gpu_lib()
 lib.cloudsc_debug_set_state_layout.argtypes = [C.c_longlong, C.c_uint]
-print("library:", os.environ.get("CLOUDSC_AMD_LIB", ca.LIB_PATH), flush=True)
+print("library:", os.environ.get("CLOUDSC_AMD_LIB", ca.LIB_PATH), " ".join(sys.argv[1:]), flush=True)
 ds = ca.load_dataset()
 VARS = (("KSEG", ca.VARIANT_KSEG), ("KCACHE", ca.VARIANT_KCACHE))
 
@@ -67,7 +67,8 @@ def rel(a, r):
 
 seq = [(-1, 0), (0, 0), (-1, 0), (4608, 0), (-1, 0), (-1, 4), (-1, 0), (-1, 0), (-1, 4), (0, 0), (-1, 0)]
 bad = 0
-for prec in (ca.FP32, ca.FP64):
+ORDER = [ca.FP64, ca.FP32] if "--fp64-first" in sys.argv else [ca.FP32, ca.FP64]
+for prec in ORDER:
     st, _ = oracle.run_oracle(ds, NG, NP, prec)
     ref = ca.state_outputs_to_template(st.arrays, NG)
     first = {}

@@ -31,9 +31,11 @@ def _worker(rank, world, port, q):
         # per-rank validation partials: field 0 gets rank-dependent numbers
         stats = [[-1.0 - rank, 1.0 + rank, 0.1 * (rank + 1), 2.0, 10.0]] + [[0.0, 0.0, 0.0, 0.0, 1.0]] * 20
         comb = ctl.gather_stats(stats)
+        # bench.py's per-rank record, gathered in rank order on every rank
+        recs = ctl.gather_records({"rank": rank, "device": rank % 1, "kernel_ms": 1.5 + rank, "col_offset": off})
         ctl.barrier()
         ctl.close()
-        q.put((rank, wall, off, n, comb[0], len(comb)))
+        q.put((rank, wall, off, n, comb[0], len(comb), recs))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, "error", repr(e)))
 
@@ -55,6 +57,8 @@ def test_gloo_world2_control_path():
     assert [(r[2], r[3]) for r in res] == [(0, 1000), (1000, 1000)]
     for r in res:
         assert r[4] == (-2.0, 2.0, 0.2, 4.0, 20.0) and r[5] == 21
+        assert r[6] == [{"rank": 0, "device": 0, "kernel_ms": 1.5, "col_offset": 0},
+                        {"rank": 1, "device": 0, "kernel_ms": 2.5, "col_offset": 1000}]
 
 
 def test_single_rank_control_is_noop():
@@ -63,6 +67,7 @@ def test_single_rank_control_is_noop():
     assert ctl.max(3.0) == 3.0
     st = [[1.0, 2.0, 3.0, 4.0, 5.0]]
     assert ctl.gather_stats(st) == [(1.0, 2.0, 3.0, 4.0, 5.0)]
+    assert ctl.gather_records({"rank": 0, "kernel_ms": 1.0}) == [{"rank": 0, "kernel_ms": 1.0}]
 
 
 def test_split_blocks_covers_columns():
