@@ -28,6 +28,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "dwarf-p-cloudsc_amd"))
 
 BYTES_PER_COL = {8: 56036, 4: 28020}     # SURVEY.md §8d algorithmic bytes per column
+# of which read (inputs incl. plude and ktype): 3701 values + 4 B; written: 3303 values
+IN_BYTES_PER_COL = {8: 3701 * 8 + 4, 4: 3701 * 4 + 4}
 HBM_PEAK_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -146,22 +148,34 @@ def roofline_traffic(ca, path, key):
         entry["kernel_source_hash"])
 
 
-def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=32, nstreams=4):
+def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
     """Host-resident block-layout arrays (pinned in place), per chunk H2D ->
-    kernel -> D2H overlapped on streams: the reference GPU drivers' TOTAL
-    semantics (cloudsc_driver.cu:344-456).  plude is restored on the host
-    between steps, outside the timed pipeline."""
-    hp = ca.HostPipeline(ds, args.ngptot, args.nproma, prec, chunk_blocks=chunk_blocks, nstreams=nstreams)
+    kernel -> D2H pipelined over an input, a kernel and an output stream: the
+    reference GPU drivers' TOTAL semantics (cloudsc_driver.cu:344-456).  plude
+    is restored on the host between steps, outside the timed pipeline.  The
+    default chunking is the measured best (profiles/r04/transfer_sweep_kseg_fp64.txt).
+    Held against the box's copy ceiling measured here (cloudsc_pcie_gbps): the
+    step moves in_bytes to the device and out_bytes back, so it takes at least
+    max(in/h2d, out/d2h, (in+out)/both)."""
+    pc = ca.pcie_gbps(0, 1 << 30, 3)
+    hp = ca.HostPipeline(ds, args.ngptot, args.nproma, prec, chunk_blocks=chunk_blocks, nstreams=slots)
     try:
         hp.run(variant)
         ms = [hp.run(variant) for _ in range(args.transfer_steps)]
     finally:
         hp.close()
     t = sum(ms) / len(ms)
+    es = 8 if prec == ca.FP64 else 4
+    # per column: 23 level inputs + plude + aerosol-free species/half/surface inputs in, outputs + plude out
+    # (the same algorithmic bytes as the roofline, split by direction: SURVEY.md §8d)
+    in_b, out_b = IN_BYTES_PER_COL[es] * args.ngptot, (BYTES_PER_COL[prec] - IN_BYTES_PER_COL[es]) * args.ngptot
+    bound_ms = 1e3 * max(in_b / (pc["h2d"] * 1e9), out_b / (pc["d2h"] * 1e9), (in_b + out_b) / (pc["both"] * 1e9))
     return {"value": round(args.ngptot / (t * 1e-3), 1), "unit": "columns/s", "ms_per_step": round(t, 3),
             "ms_per_step_min": round(min(ms), 3), "steps": len(ms),
-            "chunk_blocks": chunk_blocks, "nstreams": nstreams,
-            "bytes_per_step": BYTES_PER_COL[prec] * args.ngptot,
+            "chunk_blocks": chunk_blocks, "slots": slots, "streams": "one H2D, one kernel, one D2H",
+            "bytes_per_step": BYTES_PER_COL[prec] * args.ngptot, "bytes_in": in_b, "bytes_out": out_b,
+            "copy_ceiling_gbs": {k: round(v, 1) for k, v in pc.items()},
+            "bound_ms": round(bound_ms, 2), "frac_of_bound": round(bound_ms / t, 4),
             "note": "end-to-end TOTAL as the reference GPU drivers time it (H2D + kernel + D2H, "
                     "cloudsc_driver.cu:344,456), host-buffer path over PCIe; NOT the headline value"}
 

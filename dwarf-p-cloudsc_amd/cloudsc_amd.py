@@ -403,6 +403,7 @@ def gpu_lib(path: Optional[str] = None):
     lib.cloudsc_host_pipeline_destroy.argtypes = [C.c_void_p]
     lib.cloudsc_gpu_check.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
     lib.cloudsc_hbm_copy_gbps.argtypes = [C.c_int, C.c_longlong, C.c_int, C.POINTER(C.c_double)]
+    lib.cloudsc_pcie_gbps.argtypes = [C.c_int, C.c_longlong, C.c_int] + [C.POINTER(C.c_double)] * 3
     lib.cloudsc_cpu_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Params), C.POINTER(Fields),
                                     C.POINTER(C.c_double)]
     lib.cloudsc_debug_set_kseg_spin_limit.argtypes = [C.c_longlong]
@@ -495,6 +496,14 @@ def hbm_copy_gbps(device: int = 0, nbytes: int = 4 << 30, reps: int = 10) -> flo
     g = C.c_double()
     check(gpu_lib().cloudsc_hbm_copy_gbps(device, nbytes, reps, C.byref(g)))
     return g.value
+
+
+def pcie_gbps(device: int = 0, nbytes: int = 1 << 30, reps: int = 3) -> Dict[str, float]:
+    """Host<->device copy ceiling (cloudsc_pcie_gbps): GB/s of H2D alone, D2H
+    alone, and the total of both directions at once."""
+    h, d, b = C.c_double(), C.c_double(), C.c_double()
+    check(gpu_lib().cloudsc_pcie_gbps(device, nbytes, reps, C.byref(h), C.byref(d), C.byref(b)))
+    return {"h2d": h.value, "d2h": d.value, "both": b.value}
 
 
 def device_count() -> int:
@@ -606,7 +615,7 @@ class HostPipeline:
     copies inputs in and outputs out, chunked and overlapped over streams."""
 
     def __init__(self, ds: Dataset, ngptot: int, nproma: int = 128, precision: int = FP64, device: int = 0,
-                 chunk_blocks: int = 32, nstreams: int = 4, col_offset: int = 0, packed: bool = False):
+                 chunk_blocks: int = 128, nstreams: int = 3, col_offset: int = 0, packed: bool = False):
         """packed: all arrays carved back to back (8-byte gaps) out of ONE host
         buffer, so that neighbouring fields share pages -- the layout that
         exercises the pipeline's page-merged pinning."""

@@ -424,9 +424,22 @@ int launch_kseg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real>& p
 #endif
 }
 
+// Experiment builds (make variant VFLAGS=-DCLOUDSC_ONLY_KSEG=8 ...) instantiate
+// only the KSEG kernel of one element size without aerosols -- one kernel to
+// compile instead of twelve, for the per-phase ablation builds of
+// tools/ablation.sh; every other combination returns CLOUDSC_EINVAL.
+#ifdef CLOUDSC_ONLY_KSEG
+#define CLOUDSC_KEEP_KERNEL(real_, kseg_, aer_) (sizeof(real_) == CLOUDSC_ONLY_KSEG && (kseg_) && !(aer_))
+#else
+#define CLOUDSC_KEEP_KERNEL(real_, kseg_, aer_) true
+#endif
+
 template <typename real, bool FAST>
 int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot, int nproma, int klev,
              void* scratch, const void* plude_in, const ParamSet& ps, KsegEpoch* ep, const LaunchEvents* ev) {
+#ifdef CLOUDSC_ONLY_KSEG
+  if (variant != CLOUDSC_VARIANT_KSEG || ps.aer || sizeof(real) != CLOUDSC_ONLY_KSEG) return CLOUDSC_EINVAL;
+#endif
   KArgs<real> a = make_args<real>(f, ngptot, nproma, klev, ps);
   if (plude_in) a.plude_in = (const real*)plude_in;
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
@@ -434,8 +447,9 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
   if (aer && (!f->pre_ice || !f->picrit_aer || !f->pnice)) return CLOUDSC_EINVAL;
   int rc = CLOUDSC_OK;
   if (variant == CLOUDSC_VARIANT_KCACHE) {
-    rc = aer ? launch_kcache<real, true, FAST>(st, a, nblocks, nproma, ev)
-             : launch_kcache<real, false, FAST>(st, a, nblocks, nproma, ev);
+    if constexpr (CLOUDSC_KEEP_KERNEL(real, false, false))
+      rc = aer ? launch_kcache<real, true, FAST>(st, a, nblocks, nproma, ev)
+               : launch_kcache<real, false, FAST>(st, a, nblocks, nproma, ev);
   } else if (variant == CLOUDSC_VARIANT_KSEG) {
     if (!scratch) return CLOUDSC_EINVAL;
     PersistArgs<real> pa;
@@ -485,8 +499,11 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
     pa.base = zero_ws ? 0u : ep->base;
     pa.stamp = zero_ws ? 0u : ep->stamp;
     int grid = 0;
-    rc = aer ? launch_kseg<real, true, FAST>(st, a, pa, nproma, pa.nitems, &grid, ev)
-             : launch_kseg<real, false, FAST>(st, a, pa, nproma, pa.nitems, &grid, ev);
+    if constexpr (CLOUDSC_KEEP_KERNEL(real, true, true))
+      rc = aer ? launch_kseg<real, true, FAST>(st, a, pa, nproma, pa.nitems, &grid, ev)
+               : launch_kseg<real, false, FAST>(st, a, pa, nproma, pa.nitems, &grid, ev);
+    else if constexpr (CLOUDSC_KEEP_KERNEL(real, true, false))
+      rc = launch_kseg<real, false, FAST>(st, a, pa, nproma, pa.nitems, &grid, ev);
     if (rc) return rc;
     HIPCHK(hipGetLastError());
     if (ep) {   // the next launch on this workspace continues where this one ends
@@ -496,13 +513,17 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
     }
   } else if (variant == CLOUDSC_VARIANT_SCC_PRIVATE) {
     if (klev > kPrivKlev) return CLOUDSC_EINVAL;    // the private arrays are sized at compile time
-    if (aer) launch_physics(scc_private_entry<real, true, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
-    else launch_physics(scc_private_entry<real, false, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
+    if constexpr (CLOUDSC_KEEP_KERNEL(real, false, false)) {
+      if (aer) launch_physics(scc_private_entry<real, true, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
+      else launch_physics(scc_private_entry<real, false, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a);
+    }
   } else {
     if (!scratch) return CLOUDSC_EINVAL;
-    SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
-    if (aer) launch_physics(scc_entry<real, true, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
-    else launch_physics(scc_entry<real, false, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
+    if constexpr (CLOUDSC_KEEP_KERNEL(real, false, false)) {
+      SccScratch<real> s = scc_scratch_carve<real>((char*)scratch, nblocks, nproma, klev);
+      if (aer) launch_physics(scc_entry<real, true, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
+      else launch_physics(scc_entry<real, false, FAST>, dim3(nblocks), dim3(nproma), 0, st, ev, a, s);
+    }
   }
   if (rc) return rc;
   HIPCHK(hipGetLastError());

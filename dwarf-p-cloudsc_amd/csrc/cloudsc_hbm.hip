@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "cloudsc_amd.h"
@@ -107,4 +108,56 @@ extern "C" int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, doub
   (void)hipFree(a);
   (void)hipFree(b);
   return rc;
+}
+
+// The host<->device ceiling the host-buffer pipeline is held against (bench.py's
+// pcie_inclusive): pinned host buffers of `bytes` each way, copied by the copy
+// engines with one stream per direction (the fastest arrangement,
+// tools/pcie_probe.hip: 97 GB/s both ways at once against 65-85 GB/s with 2-8
+// streams per direction), in 64 MiB pieces; H2D alone, D2H alone, and both at
+// once (total of the two directions); best of `reps` after one warm-up each.
+extern "C" int cloudsc_pcie_gbps(int device, long long bytes, int reps, double* h2d, double* d2h, double* both) {
+  if (!h2d || !d2h || !both || bytes < (1 << 20) || reps <= 0) return CLOUDSC_EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CLOUDSC_ENODEV;
+  HIPCHK(hipSetDevice(device));
+  const size_t nb = (size_t)bytes;
+  char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  hipError_t e = hipHostMalloc((void**)&h_in, nb, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&h_out, nb, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_in, nb);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_out, nb);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMemset(d_out, 1, nb);
+  if (e == hipSuccess) std::fill(h_in, h_in + nb, (char)2);
+  const size_t piece = (size_t)64 << 20;
+  double best[3] = {0, 0, 0};
+  for (int dir = 1; dir <= 3 && e == hipSuccess; dir++) {
+    for (int r = -1; r < reps && e == hipSuccess; r++) {
+      e = hipDeviceSynchronize();
+      const auto t0 = std::chrono::steady_clock::now();
+      for (size_t off = 0; off < nb && e == hipSuccess; off += piece) {
+        const size_t len = std::min(piece, nb - off);
+        if (dir & 1) e = hipMemcpyAsync(d_in + off, h_in + off, len, hipMemcpyHostToDevice, s_in);
+        if ((dir & 2) && e == hipSuccess) e = hipMemcpyAsync(h_out + off, d_out + off, len, hipMemcpyDeviceToHost, s_out);
+      }
+      if (e == hipSuccess) e = hipDeviceSynchronize();
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      const double gbs = (dir == 3 ? 2.0 : 1.0) * (double)nb / s / 1e9;
+      if (r >= 0 && gbs > best[dir - 1]) best[dir - 1] = gbs;
+    }
+  }
+  if (s_in) (void)hipStreamDestroy(s_in);
+  if (s_out) (void)hipStreamDestroy(s_out);
+  if (d_in) (void)hipFree(d_in);
+  if (d_out) (void)hipFree(d_out);
+  if (h_in) (void)hipHostFree(h_in);
+  if (h_out) (void)hipHostFree(h_out);
+  if (e != hipSuccess) return hip_fail(e, "pcie copy measurement");
+  *h2d = best[0];
+  *d2h = best[1];
+  *both = best[2];
+  return CLOUDSC_OK;
 }

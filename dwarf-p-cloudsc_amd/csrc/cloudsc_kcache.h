@@ -324,6 +324,32 @@ CLOUDSC_HD void init_level(const P& c, const LevelIn<real>& in, LevelState<real>
   s.qtend = qtend;
 }
 
+// Per-phase cost ablation (timing-only experiment builds, tools/ablation.sh):
+// -DCLOUDSC_ABLATE=<mask> skips the marked sections of the physics; the loads
+// and stores stay, downstream sections see zero contributions (or, for the
+// Newton chain, a cheap stand-in of the same sign), so the difference to the
+// full kernel is the section's cost.  0 (the default) compiles nothing out.
+#ifndef CLOUDSC_ABLATE
+#define CLOUDSC_ABLATE 0
+#endif
+enum AblateBit : unsigned {
+  AB_SUPSAT = 1u << 0,     // 3.1 supersaturation adjustment
+  AB_CONV = 1u << 1,       // 3.2 detrainment, 3.3 subsidence source and sink
+  AB_EROSION = 1u << 2,    // 3.4 erosion
+  AB_NEWTON = 1u << 3,     // 3.4 dqs/dt: the two Newton steps
+  AB_COND = 1u << 4,       // 3.4a/b evaporation, condensation, new clouds
+  AB_DEPOS = 1u << 5,      // 3.7 ice deposition
+  AB_SEDIM = 1u << 6,      // 4.2 sedimentation, precipitation cover
+  AB_AUTO = 1u << 7,       // 4.3 autoconversion (snow, KK rain), riming
+  AB_MELT = 1u << 8,       // 4.4 melting, freezing
+  AB_EVAP = 1u << 9,       // 4.5 rain and snow evaporation
+  AB_TRUNC = 1u << 10,     // 5.2 sink truncation
+  AB_SOLVE = 1u << 11,     // 5.2.2 implicit solver (divisions and substitutions)
+  AB_SAT = 1u << 12,       // saturation exponentials at T (e_liq, e_ice): cheap stand-ins
+};
+constexpr unsigned kAblate = CLOUDSC_ABLATE;
+#define CLOUDSC_RUN(bit) ((kAblate & (bit)) == 0)
+
 // ===== 3.-6. physics of one level ncldtop <= k (cloudsc_c.c:732-2508) =====
 // Nothing to do at the middle of a level (the default hook of physics_level).
 struct NoMidHook {
@@ -352,7 +378,8 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     const real pap_k = in.pap;
     // saturation values (:583-609)
-    const real e_liq = exp_liq<real>(c, ztp1), e_ice = exp_ice<real>(c, ztp1);
+    const real e_liq = CLOUDSC_RUN(AB_SAT) ? exp_liq<real>(c, ztp1) : launder_vgpr(ztp1 * R(0.02));
+    const real e_ice = CLOUDSC_RUN(AB_SAT) ? exp_ice<real>(c, ztp1) : launder_vgpr(ztp1 * R(0.019));
     // divisors shared by several divisions (cl_recip: one reciprocal, same quotient bits)
     const Recip<real> r_pap = cl_recip_p<real>(c, pap_k);
     const real zfoeewmt = fmin(cl_div_p<real>(c, (c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)), r_pap), R(0.5));
@@ -428,8 +455,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       zfac = za + zfokoop * (R(1.0) - za);
       zfaci = c.zfaci_koop;
     }
-    real zsupsat;
-    if (za > c.one_m_ramin) {
+    real zsupsat = R(0.0);
+    if (!CLOUDSC_RUN(AB_SUPSAT)) {
+    } else if (za > c.one_m_ramin) {
       zsupsat = fmax(cl_div_p<real>(c, (zqx[QV] - zfac * zqsice), zcorqsice), R(0.0));
     } else {
       const real zqp1env = cl_div_p<real>(c, (zqx[QV] - za * zqsice), fmax(R(1.0) - za, zepsilon));
@@ -442,7 +470,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
       zsolac = (R(1.0) - za) * zfaci;
     }
-    if (in.psupsat > zepsec) {
+    if (CLOUDSC_RUN(AB_SUPSAT) && in.psupsat > zepsec) {
       if (warm_homo) {
         sa_ll = sa_ll + in.psupsat; psup_l = in.psupsat; zqxfg[QL] = zqxfg[QL] + in.psupsat;
       } else {
@@ -452,7 +480,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
 
     // 3.2 detrainment from convection (:967-987)
-    if (k < klev - 1) {
+    if (CLOUDSC_RUN(AB_CONV) && k < klev - 1) {
       plude_k = plude_k * zdtgdp;
       if (nb.plu_n > zepsec && plude_k > c.rlmin) {
         zsolac = zsolac + cl_div_p<real>(c, plude_k, nb.plu_n);
@@ -467,7 +495,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
 
     // 3.3 subsidence source from the layer above + evaporation (:1002-1058)
-    if (k > ncldtop0) {
+    if (CLOUDSC_RUN(AB_CONV) && k > ncldtop0) {
       const real zmf = fmax(R(0.0), (nb.pmfu_k + nb.pmfd_k) * zdtgdp);
       real zacust = zmf * cs.zanewm1;
       const real zlcust_l = zmf * cs.qxnm1_l;
@@ -497,7 +525,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
 
     // subsidence sink of cloud to the layer below (:1064-1075)
-    if (k < klev - 1) {
+    if (CLOUDSC_RUN(AB_CONV) && k < klev - 1) {
       const real zmfdn = fmax(R(0.0), (nb.pmfu_n + nb.pmfd_n) * zdtgdp);
       zsolab = zsolab + zmfdn;
       sb_ll = sb_ll + zmfdn;
@@ -507,7 +535,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     // 3.4 erosion of clouds by turbulent mixing (:1087-1118)
     const real zldifdt = (cc.ktype > 0 && plude_k > zepsec) ? pval(c, c.zldifdt_conv) : pval(c, c.zldifdt0);
-    if (zli > zepsec) {
+    if (CLOUDSC_RUN(AB_EROSION) && zli > zepsec) {
       const real ze = zldifdt * fmax(zqsmix - zqx[QV], R(0.0));
       real zleros = za * ze;
       zleros = fmin(zleros, zevaplimmix);
@@ -520,7 +548,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     // 3.4 condensation/evaporation due to dqsat/dt: two Newton steps (:1137-1182)
     real zdqs;
-    {
+    if (!CLOUDSC_RUN(AB_NEWTON)) {
+      zdqs = launder_vgpr((zqsmix - zqx[QV]) * R(0.1));   // stand-in of the right sign
+    } else {
       const real zdtdp = cl_div_p<real>(c, (c.zrdcp * ztp1), r_pap);
       const real zdpmxdt = zdp * c.zqtmst;
       const real zmfdn = (k < klev - 1) ? nb.pmfu_n + nb.pmfd_n : R(0.0);
@@ -547,7 +577,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
 
     // 3.4a evaporation of clouds (:1189-1207)
-    if (zdqs > R(0.0)) {
+    if (CLOUDSC_RUN(AB_COND) && zdqs > R(0.0)) {
       real zlevap = za * fmin(zdqs, zlicld);
       zlevap = fmin(zlevap, zevaplimmix);
       zlevap = fmin(zlevap, fmax(zqsmix - zqx[QV], R(0.0)));
@@ -555,7 +585,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       sa_iv = sa_iv + zicefrac * zlevap;
     }
     // 3.4b(1) increase of cloud water in existing clouds (:1213-1250)
-    if (zdqs <= -c.rlmin && za > zepsec) {
+    if (CLOUDSC_RUN(AB_COND) && zdqs <= -c.rlmin && za > zepsec) {
       real zlcond1 = fmax(-zdqs, R(0.0));
       real zcdmax;
       if (za > R(0.99)) {
@@ -572,7 +602,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
     }
     // 3.4b(2) generation of new clouds (:1253-1363)
-    if (zdqs <= -c.rlmin && za < R(1.0) - zepsec) {
+    if (CLOUDSC_RUN(AB_COND) && zdqs <= -c.rlmin && za < R(1.0) - zepsec) {
       real zrhc = c.ramid;
       const real zsigk = cl_div_p<real>(c, pap_k, cc.paph_sfc);
       if (zsigk > R(0.8)) {
@@ -614,7 +644,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // 3.7 growth of ice by vapour deposition, Rotstayn (:1382-1447)
     if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
     else cs.zcldtopdist = cs.zcldtopdist + cl_div_p<real>(c, zdp, (zrho * c.rg));
-    if (zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
+    if (CLOUDSC_RUN(AB_DEPOS) && zqxfg[QL] > c.rlmin && ztp1 < c.rtt) {
       const real zvpice = cl_div_known_p<real>(c, ((c.r2es * e_ice) * c.rv), c.rd, c.rd_rcp);
       const real zvpliq = zvpice * zfokoop;
       const real zicenuclei = R(1000.0) * cl_exp<real>(c, cl_div_p<real>(c, (R(12.96) * (zvpliq - zvpice)), zvpliq) - R(0.639));
@@ -638,7 +668,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     zlicld = zliqcld + zicecld;
 
     // 4.2 sedimentation of ice, rain, snow (:1541-1576)
-    if (k > ncldtop0) {
+    if (CLOUDSC_RUN(AB_SEDIM) && k > ncldtop0) {
       fsrc_i = cs.pfx_i * zdtgdp; sa_ii = sa_ii + fsrc_i; zqxfg[QI] = zqxfg[QI] + fsrc_i; zqpretot = zqpretot + zqxfg[QI];
       fsrc_r = cs.pfx_r * zdtgdp; sa_rr = sa_rr + fsrc_r; zqxfg[QR] = zqxfg[QR] + fsrc_r; zqpretot = zqpretot + zqxfg[QR];
       fsrc_s = cs.pfx_s * zdtgdp; sa_ss = sa_ss + fsrc_s; zqxfg[QS] = zqxfg[QS] + fsrc_s; zqpretot = zqpretot + zqxfg[QS];
@@ -650,7 +680,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     // precip cover overlap, MAX-RAN (:1594-1611)
     real zcovpclr, zraincld, zsnowcld;
-    if (zqpretot > zepsec) {
+    if (CLOUDSC_RUN(AB_SEDIM) && zqpretot > zepsec) {
       cs.zcovptot = R(1.0) - cl_div_p<real>(c, (R(1.0) - cs.zcovptot) * (R(1.0) - fmax(za, cs.a_prev)), (R(1.0) - fmin(cs.a_prev, R(1.0) - R(1.0e-6))));
       cs.zcovptot = fmax(cs.zcovptot, c.rcovpmin);
       zcovpclr = fmax(R(0.0), cs.zcovptot - za);
@@ -663,7 +693,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     const bool cold = ztp1 <= c.rtt;
     // 4.3a autoconversion to snow (:1616-1637)
-    if (cold && zicecld > zepsec) {
+    if (CLOUDSC_RUN(AB_AUTO) && cold && zicecld > zepsec) {
       real zzco = c.zzco_snow * cl_exp<real>(c, c.rsnowlin2 * (ztp1 - c.rtt));
       real zlcrit = pval(c, c.rlcritsnow);
       if (c.laericeauto) {
@@ -674,7 +704,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       sb_is = sb_is + zzco * (R(1.0) - cl_exp<real>(c, -(r * r)));
     }
     // 4.3b warm rain, Khairoutdinov and Kogan 2000 (:1644-1761)
-    if (zliqcld > zepsec) {
+    if (CLOUDSC_RUN(AB_AUTO) && zliqcld > zepsec) {
       real zrainaut = R(0.0), zrainacc = R(0.0);
       if (zliqcld > cc.kk_lcrit) {
         zrainaut = ((((R(1.5) * za) * c.ptsphy) * c.rcl_kkaau) * cl_pow<real>(c, zliqcld, c.rcl_kkbauq)) * cc.kk_pow;
@@ -691,7 +721,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
     }
     // riming of snow by cloud water (:1768-1808)
-    if (cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) {
+    if (CLOUDSC_RUN(AB_AUTO) && cold && zliqcld > zepsec && cs.zcovptot > R(0.01) && zsnowcld > zepsec) {
       const real zfallcorr = cl_pow<real>(c, cl_div_p<real>(c, c.rdensref, zrho), R(0.4));
       real zsnowrime = ((((R(0.3) * cs.zcovptot) * c.ptsphy) * c.rcl_const7s) * zfallcorr) *
                        cl_pow<real>(c, (zrho * zsnowcld) * c.rcl_const1s, c.rcl_const8s);
@@ -701,7 +731,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     // 4.4a melting of snow and ice (:1817-1859)
     const real zicetot = zqxfg[QI] + zqxfg[QS];
-    if (zicetot > zepsec && ztp1 > c.rtt) {
+    if (CLOUDSC_RUN(AB_MELT) && zicetot > zepsec && ztp1 > c.rtt) {
       const real zsubsat = fmax(zqsice - zqx[QV], R(0.0));
       const real ztdmtw0 = ztp1 - c.rtt - zsubsat * (ztw1 + ztw2 * (pap_k - ztw3) - ztw4 * (ztp1 - ztw5));
       const real zcons1 = fabs(cl_div_known_p<real>(c, (c.ptsphy * (R(1.0) + R(0.5) * ztdmtw0)), c.rtaumel, c.rtaumel_rcp));
@@ -723,7 +753,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     }
 
     // 4.4b freezing of rain (:1864-1908)
-    if (zqx[QR] > zepsec) {
+    if (CLOUDSC_RUN(AB_MELT) && zqx[QR] > zepsec) {
       if (cold && cs.t_prev > c.rtt) {
         const real tot = fmax(zqx[QS] + zqx[QR], zepsec);
         cs.rainfrac = cl_div_p<real>(c, zqx[QR], tot);
@@ -747,7 +777,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     // 4.4c freezing of liquid (:1913-1928)
     {
       const real zfrzmax = fmax((c.rthomo - ztp1) * c.zrldcp, R(0.0));
-      if (zfrzmax > zepsec && zqxfg[QL] > zepsec) {
+      if (CLOUDSC_RUN(AB_MELT) && zfrzmax > zepsec && zqxfg[QL] > zepsec) {
         const real zfrz = fmin(zqxfg[QL], zfrzmax);
         sa_li = sa_li + zfrz;
       }
@@ -761,7 +791,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     auto zzrh0_of = [&]() {
       return fmin(fmax(c.rprecrhmax + cl_div_p<real>(c, ((R(1.0) - c.rprecrhmax) * cs.zcovpmax), r_1mza), c.rprecrhmax), R(1.0));
     };
-    if (zcovpclr > zepsec && zqxfg[QR] > zepsec) {
+    if (CLOUDSC_RUN(AB_EVAP) && zcovpclr > zepsec && zqxfg[QR] > zepsec) {
       const real zfoeeliqt = fmin(cl_div_p<real>(c, (c.r2es * e_liq), r_pap), R(0.5));
       const real zqsliq = cl_div_p<real>(c, zfoeeliqt, (R(1.0) - c.retv * zfoeeliqt));
       const real zzrh = fmin(R(0.8), zzrh0_of());
@@ -785,7 +815,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
     }
     // 4.5 evaporation of snow, Sundqvist (:2048-2087)
-    if (zcovpclr > zepsec && zqxfg[QS] > zepsec) {
+    if (CLOUDSC_RUN(AB_EVAP) && zcovpclr > zepsec && zqxfg[QS] > zepsec) {
       const real zzrh = zzrh0_of();
       real zqe = cl_div_p<real>(c, (zqx[QV] - za * zqsice), r_1mza);
       zqe = fmax(R(0.0), fmin(zqe, zqsice));
@@ -834,7 +864,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       psum = R(0.0) + sa_ll; psum = psum + (-sa_li); psum = psum + (-sa_lr); psum = psum + (-sa_ls); psum = psum + (-sa_lv);
       {
         const real zmm = fmax(zqx[QL], zepsec), den = fmax(R(0.0) - psum, zmm);
-        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+        if (CLOUDSC_RUN(AB_TRUNC) && (den != zmm || zmm == (real)__builtin_inf())) {   // else zrat = 1: identity
           zrat = cl_div_p<real>(c, zmm, den);
           if (sa_ll < R(0.0)) { sa_ll = sa_ll * zrat; sa_ll = sa_ll * zrat; }
           if (-sa_li < R(0.0)) sa_li = sa_li * zrat;
@@ -847,7 +877,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       psum = R(0.0) + sa_li; psum = psum + sa_ii; psum = psum + (-sa_ir); psum = psum + z; psum = psum + (-sa_iv);
       {
         const real zmm = fmax(zqx[QI], zepsec), den = fmax(R(0.0) - psum, zmm);
-        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+        if (CLOUDSC_RUN(AB_TRUNC) && (den != zmm || zmm == (real)__builtin_inf())) {   // else zrat = 1: identity
           zrat = cl_div_p<real>(c, zmm, den);
           if (sa_li < R(0.0)) sa_li = sa_li * zrat;
           if (sa_ii < R(0.0)) { sa_ii = sa_ii * zrat; sa_ii = sa_ii * zrat; }
@@ -859,7 +889,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       psum = R(0.0) + sa_lr; psum = psum + sa_ir; psum = psum + sa_rr; psum = psum + sa_sr; psum = psum + (-sa_rv);
       {
         const real zmm = fmax(zqx[QR], zepsec), den = fmax(R(0.0) - psum, zmm);
-        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+        if (CLOUDSC_RUN(AB_TRUNC) && (den != zmm || zmm == (real)__builtin_inf())) {   // else zrat = 1: identity
           zrat = cl_div_p<real>(c, zmm, den);
           if (sa_lr < R(0.0)) sa_lr = sa_lr * zrat;
           if (sa_ir < R(0.0)) sa_ir = sa_ir * zrat;
@@ -872,7 +902,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       psum = R(0.0) + sa_ls; psum = psum + z; psum = psum + (-sa_sr); psum = psum + sa_ss; psum = psum + (-sa_sv);
       {
         const real zmm = fmax(zqx[QS], zepsec), den = fmax(R(0.0) - psum, zmm);
-        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+        if (CLOUDSC_RUN(AB_TRUNC) && (den != zmm || zmm == (real)__builtin_inf())) {   // else zrat = 1: identity
           zrat = cl_div_p<real>(c, zmm, den);
           if (sa_ls < R(0.0)) sa_ls = sa_ls * zrat;
           if (-sa_sr < R(0.0)) sa_sr = sa_sr * zrat;
@@ -884,7 +914,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       psum = R(0.0) + sa_lv; psum = psum + sa_iv; psum = psum + sa_rv; psum = psum + sa_sv; psum = psum + z;
       {
         const real zmm = fmax(zqx[QV], zepsec), den = fmax(R(0.0) - psum, zmm);
-        if (den != zmm || zmm == (real)__builtin_inf()) {   // else zrat = zmm/zmm = 1: the scaling is an identity
+        if (CLOUDSC_RUN(AB_TRUNC) && (den != zmm || zmm == (real)__builtin_inf())) {   // else zrat = 1: identity
           zrat = cl_div_p<real>(c, zmm, den);
           if (sa_lv < R(0.0)) sa_lv = sa_lv * zrat;
           if (sa_iv < R(0.0)) sa_iv = sa_iv * zrat;
@@ -932,10 +962,12 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       // back substitution (step 2): vapour and the diagonal solves
       // qn_v = qn_v / zqlhs[qv][qv] with a pivot of exactly 1: x / 1 == x in IEEE arithmetic
       // (signed zeros and NaN included), so the division is dropped
-      qn_s = cl_div_p<real>(c, qn_s, d_s);
-      qn_r = cl_div_p<real>(c, qn_r, d_r);
-      qn_i = cl_div_p<real>(c, qn_i, r_di);
-      qn_l = cl_div_p<real>(c, qn_l, r_dl);
+      if (CLOUDSC_RUN(AB_SOLVE)) {
+        qn_s = cl_div_p<real>(c, qn_s, d_s);
+        qn_r = cl_div_p<real>(c, qn_r, d_r);
+        qn_i = cl_div_p<real>(c, qn_i, r_di);
+        qn_l = cl_div_p<real>(c, qn_l, r_dl);
+      }
       // no small values (:2402-2412)
       if (qn_l < zepsec) { qn_v = qn_v + qn_l; qn_l = R(0.0); }
       if (qn_i < zepsec) { qn_v = qn_v + qn_i; qn_i = R(0.0); }

@@ -23,9 +23,16 @@ using namespace cloudsc_impl;
 // run, and copy the outputs back (cloudsc_driver.cu:344-456; the "field"
 // variant of README.md:311-330 overlaps them).  Here the blocks are cut into
 // chunks of `chunk_blocks` NPROMA blocks -- one contiguous range of every
-// field, because the layout is block-major -- and chunk c runs on stream
-// c % nstreams: H2D of its inputs, the kernel, D2H of its outputs.  The host
-// arrays are pinned in place (hipHostRegister) once, at creation.
+// field, because the layout is block-major -- and chunk c uses device buffer
+// slot c % nslots.  Three streams form the pipeline (round 4): one carries every
+// host-to-device copy, one every kernel, one every device-to-host copy, ordered
+// per slot by events -- the inputs of chunk c go in while chunk c-1 computes and
+// chunk c-2's outputs come out.  One stream per direction is what the copy
+// engines run fastest: 97 GB/s both directions together with one stream each,
+// 65-85 GB/s with 2-8 streams per direction (tools/pcie_probe.hip,
+// profiles/r04/pcie_probe.jsonl; round 3 ran H2D, kernel and D2H of a chunk on
+// one of 4 streams: 74 GB/s).  The host arrays are pinned in place
+// (hipHostRegister) once, at creation.
 //
 // Pinning is by whole pages, and arrays from a general-purpose allocator share
 // pages (the end of one field and the start of the next).  Registering each
@@ -72,18 +79,19 @@ size_t per_block_elems(int kind, int nproma, int klev) {
 }  // namespace
 
 struct cloudsc_host_pipeline {
-  int device, precision, ngptot, nproma, klev, nblocks, chunk_blocks, nstreams;
+  int device, precision, ngptot, nproma, klev, nblocks, chunk_blocks, nstreams;   // nstreams: device slots
   size_t es;
   cloudsc_fields_t host;
   std::vector<void*> pinned;
   struct Slot {
-    hipStream_t st = nullptr;
     cloudsc_fields_t dev{};
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
     int scratch_variant = 0;
+    hipEvent_t in_done = nullptr, k_done = nullptr, out_done = nullptr;   // the slot's last chunk, per stage
   };
   std::vector<Slot> slots;
+  hipStream_t st_in = nullptr, st_k = nullptr, st_out = nullptr;
   std::vector<void*> allocs;
   ParamSet params;          // snapshot of the device's default set at creation
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -174,9 +182,14 @@ int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int 
   if ((rc = param_set_copy(&p->params, device_default_params(device)))) return fail(rc);
   void* const* hf = (void* const*)&p->host;
   if ((rc = pin_host_fields(p, hf))) return fail(rc);
-  p->slots.resize(nstreams);
+  for (hipStream_t* q : {&p->st_in, &p->st_k, &p->st_out})
+    if (hipStreamCreateWithFlags(q, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
+  // more slots than chunks would never be used
+  const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
+  p->slots.resize(nstreams < nchunks ? nstreams : nchunks);
   for (auto& s : p->slots) {
-    if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
+    for (hipEvent_t* e : {&s.in_done, &s.k_done, &s.out_done})
+      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return fail(CLOUDSC_EHIP);
     void** df = (void**)&s.dev;
     for (int i = 0; i < kNumFields; i++) {
       if (!hf[i]) continue;
@@ -201,6 +214,7 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
   HIPCHK(hipSetDevice(p->device));
   const int vk = variant_kind(variant);   // without the option bits
   const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
+  const int nslots = (int)p->slots.size();
   // workspaces for the chunk size (SCC / KSEG), allocated on first use
   for (auto& s : p->slots) {
     if (vk == CLOUDSC_VARIANT_KCACHE || vk == CLOUDSC_VARIANT_SCC_PRIVATE || s.scratch_variant == vk) continue;
@@ -217,40 +231,52 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
     s.scratch_variant = vk;
   }
   const void* const* hf = (const void* const*)&p->host;
-  // all streams start after ev0 (recorded on the null stream) and ev1 waits for all of them
+  // the three streams start after ev0 (recorded on the null stream) and ev1 waits for all of them
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipEventRecord(p->ev0, nullptr));
-  for (auto& s : p->slots) HIPCHK(hipStreamWaitEvent(s.st, p->ev0, 0));
+  for (hipStream_t q : {p->st_in, p->st_k, p->st_out}) HIPCHK(hipStreamWaitEvent(q, p->ev0, 0));
   for (int c = 0; c < nchunks && rc == CLOUDSC_OK; c++) {
-    auto& s = p->slots[c % p->nstreams];
+    auto& s = p->slots[c % nslots];
+    const bool reuse = c >= nslots;        // the slot held chunk c - nslots
     const int b0 = c * p->chunk_blocks;
     const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
     const long long col0 = (long long)b0 * p->nproma;
     const int ncols = (int)((col0 + (long long)nb * p->nproma <= p->ngptot) ? (long long)nb * p->nproma
                                                                             : p->ngptot - col0);
     void* const* df = (void* const*)&s.dev;
+    // inputs: after the slot's previous kernel has read its inputs
+    if (reuse) HIPCHK(hipStreamWaitEvent(p->st_in, s.k_done, 0));
     for (int i = 0; i < kNumFields; i++) {
       const FieldDesc& d = kFieldTable[i];
       if (!hf[i] || d.dir == FD_OUT) continue;
       const size_t eb = d.is_int ? sizeof(int) : p->es;
       const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * eb;
       HIPCHK(hipMemcpyAsync(df[i], (const char*)hf[i] + (size_t)b0 * per, (size_t)nb * per, hipMemcpyHostToDevice,
-                            s.st));
+                            p->st_in));
     }
-    rc = gpu_run_impl(p->device, s.st, p->precision, variant, ncols, p->nproma, p->klev, &s.dev, s.scratch, nullptr,
-                      &p->params);
+    HIPCHK(hipEventRecord(s.in_done, p->st_in));
+    // kernel: after its inputs are in and the slot's previous outputs are out
+    HIPCHK(hipStreamWaitEvent(p->st_k, s.in_done, 0));
+    if (reuse) HIPCHK(hipStreamWaitEvent(p->st_k, s.out_done, 0));
+    rc = gpu_run_impl(p->device, p->st_k, p->precision, variant, ncols, p->nproma, p->klev, &s.dev, s.scratch,
+                      nullptr, &p->params);
     if (rc) break;
+    HIPCHK(hipEventRecord(s.k_done, p->st_k));
+    // outputs (and plude): after the kernel
+    HIPCHK(hipStreamWaitEvent(p->st_out, s.k_done, 0));
     for (int i = 0; i < kNumFields; i++) {
       const FieldDesc& d = kFieldTable[i];
       if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
       const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * p->es;
-      HIPCHK(hipMemcpyAsync((char*)hf[i] + (size_t)b0 * per, df[i], (size_t)nb * per, hipMemcpyDeviceToHost, s.st));
+      HIPCHK(hipMemcpyAsync((char*)hf[i] + (size_t)b0 * per, df[i], (size_t)nb * per, hipMemcpyDeviceToHost,
+                            p->st_out));
     }
+    HIPCHK(hipEventRecord(s.out_done, p->st_out));
   }
-  for (auto& s : p->slots) {
+  for (hipStream_t q : {p->st_in, p->st_k, p->st_out}) {
     hipEvent_t e;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(e, s.st));
+    HIPCHK(hipEventRecord(e, q));
     HIPCHK(hipStreamWaitEvent(nullptr, e, 0));
     (void)hipEventDestroy(e);
   }
@@ -258,11 +284,11 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
   HIPCHK(hipEventSynchronize(p->ev1));
   if (rc) return rc;
   // KSEG: a timed-out segment hand-off in any chunk invalidates the step (the
-  // error word of a slot's workspace accumulates over its chunks)
-  // (every slot's word is read and cleared, also after the first failure)
+  // error word of a slot's workspace accumulates over its chunks; every slot's
+  // word is read and cleared, also after the first failure)
   if (vk == CLOUDSC_VARIANT_KSEG)
     for (auto& s : p->slots) {
-      const int r = kseg_check(p->device, s.st, s.scratch);
+      const int r = kseg_check(p->device, p->st_k, s.scratch);
       if (r && !rc) rc = r;
     }
   if (rc) return rc;
@@ -275,8 +301,11 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
 int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p) {
   if (!p) return CLOUDSC_EINVAL;
   (void)hipSetDevice(p->device);
+  for (hipStream_t q : {p->st_in, p->st_k, p->st_out})
+    if (q) { (void)hipStreamSynchronize(q); (void)hipStreamDestroy(q); }
   for (auto& s : p->slots)
-    if (s.st) { (void)hipStreamSynchronize(s.st); (void)hipStreamDestroy(s.st); }
+    for (hipEvent_t e : {s.in_done, s.k_done, s.out_done})
+      if (e) (void)hipEventDestroy(e);
   for (void* q : p->allocs) (void)hipFree(q);
   for (void* h : p->pinned) (void)hipHostUnregister(h);
   param_set_free(&p->params);

@@ -136,13 +136,19 @@ void* const* valid_slot(const cloudsc_gpu_state* s, int id, int* kind) {
   return slots[id];
 }
 
-// diagnostic allocation flags of the state's fields (cloudsc_debug_set_state_layout,
-// hipExtMallocWithFlags); 0 = hipMalloc
+#ifdef CLOUDSC_DEBUG_KNOBS
+// diagnostic build only: allocation flags of the state's fields
+// (cloudsc_debug_set_state_layout, hipExtMallocWithFlags); 0 = hipMalloc
 std::atomic<unsigned> g_alloc_flags{0};
+#endif
 
 int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
+#ifdef CLOUDSC_DEBUG_KNOBS
   const unsigned fl = g_alloc_flags.load();
   hipError_t e = fl ? hipExtMallocWithFlags(p, bytes, fl) : hipMalloc(p, bytes);
+#else
+  hipError_t e = hipMalloc(p, bytes);
+#endif
   if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
   s->allocs.push_back(*p);
   return CLOUDSC_OK;
@@ -289,17 +295,27 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
 }
 
 int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags) {
-  // Round 3 refused alloc_flags after states created behind a destroyed
-  // hipDeviceMallocContiguous state computed wrong values.  The cause was the
-  // parameter upload (a null-stream hipMemcpy from pageable memory, unordered
-  // with the launches on the state's non-blocking stream, fixed in
-  // param_set_upload): with that upload re-introduced the failure reappears,
-  // in KCACHE as in KSEG, and with the ordered upload 44 of 44 runs of the same
-  // sequence are bit-exact to the oracle (profiles/r04/contiguous_alloc_hazard.txt).
+  // Allocation flags are refused by the product library (the diagnostic build,
+  // -DCLOUDSC_DEBUG_KNOBS, admits them to reproduce the following).  After
+  // states whose fields were hipDeviceMallocContiguous allocations had been
+  // destroyed, later states computed wrong values.  Two causes were found
+  // (profiles/r04/contiguous_alloc_hazard.txt): the round-3 parameter upload
+  // (a null-stream hipMemcpy from pageable memory, unordered with the launches;
+  // fixed in param_set_upload -- re-introducing it makes the failure reappear),
+  // and a second one that remains with the fix in one order of states: the
+  // input fields of a new state (plain hipMalloc) hold wrong words right after
+  // its expansion, with no live allocations overlapping, also with every kernel
+  // and copy serialized (AMD_SERIALIZE_KERNEL/COPY=3), KCACHE as KSEG; a
+  // standalone HIP program with the same allocation pattern does not reproduce
+  // it.  Unexplained; the library never allocates with flags.
   // A stagger must keep every field aligned for the widest element (a multiple
   // of 256 bytes) and is taken modulo the 2 MiB arena alignment.
   if (stagger >= 0 && stagger % 256 != 0) return CLOUDSC_EINVAL;
+#ifdef CLOUDSC_DEBUG_KNOBS
   g_alloc_flags.store(alloc_flags);
+#else
+  if (alloc_flags != 0) return CLOUDSC_EINVAL;
+#endif
   g_layout_stagger.store(stagger < 0 ? -1 : stagger % (long long)kArenaAlign);
   return CLOUDSC_OK;
 }

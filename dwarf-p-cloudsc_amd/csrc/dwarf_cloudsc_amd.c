@@ -111,7 +111,7 @@ static void usage(const char *prog) {
           "  --transfer            host-buffer path: block-layout arrays in host memory,\n"
           "                        H2D -> kernel -> D2H per chunk, overlapped on streams\n"
           "                        (TOTAL includes the transfers, like cloudsc_driver.cu)\n"
-          "  --chunk B --streams S chunk size in NPROMA blocks (32) and streams (4)\n"
+          "  --chunk B --streams S chunk size in NPROMA blocks (128) and device chunk slots (3)\n"
           "  --write-h5 DIR        write DIR/input.h5 and DIR/reference.h5 of the loaded\n"
           "                        dataset and exit\n",
           prog);
@@ -122,7 +122,7 @@ static int parse(int argc, char **argv, options_t *o) {
   o->numomp = 1; o->ngptot = 100; o->nproma = 4;     /* dwarf_cloudsc.c:25-27 defaults */
   o->ngpus = 1; o->precision = CLOUDSC_FP64; o->variant = CLOUDSC_VARIANT_KSEG;
   o->reps = 1; o->warmup = 1; o->tol = 10.0 * DBL_EPSILON;
-  o->chunk_blocks = 32; o->nstreams = 4;   /* profiles/r01/transfer_sweep_kseg_fp64.jsonl */
+  o->chunk_blocks = 128; o->nstreams = 3;  /* chunk slots; profiles/r04/transfer_sweep_kseg_fp64.txt */
   int npos = 0;
   long pos[3] = {0, 0, 0};
   for (int i = 1; i < argc; i++) {

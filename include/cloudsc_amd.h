@@ -211,11 +211,11 @@ int cloudsc_debug_set_kseg_schedule(int nseg, int grid);
  * 2 MiB -- for measuring how the HBM placement of the ~47 concurrently
  * streamed fields affects the kernel time (tools/ab_layout.py).  stagger must
  * be a multiple of 256 bytes (CLOUDSC_EINVAL otherwise) and is taken modulo
- * 2 MiB.  alloc_flags != 0: the state's allocations are made with
- * hipExtMallocWithFlags(alloc_flags) (e.g. 4 = hipDeviceMallocContiguous).
- * (Round 3 refused the flags after wrong values in states created behind a
- * destroyed contiguous state; the cause was an unordered parameter upload,
- * fixed: profiles/r04/contiguous_alloc_hazard.txt.) */
+ * 2 MiB.  alloc_flags must be 0 (CLOUDSC_EINVAL otherwise): states created
+ * after destroyed states whose fields were hipDeviceMallocContiguous
+ * allocations computed wrong values -- in part the round-3 parameter-upload
+ * race (fixed), in part a cause not found (profiles/r04/contiguous_alloc_hazard.txt);
+ * the diagnostic build (-DCLOUDSC_DEBUG_KNOBS) admits the flags to reproduce it. */
 int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags);
 
 /* Diagnostic: the kernels' single-precision exp/pow on the device, element-wise
@@ -233,6 +233,13 @@ const char *cloudsc_last_hip_error(void);
  * of `reps` launches after one warm-up, in GB/s (10^9 B/s).  bench.py reports
  * it as roofline.achievable_peak beside the 8 TB/s spec. */
 int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, double *gbps);
+
+/* Measurement: the host<->device copy ceiling of this device, the bound of the
+ * host-buffer pipeline: `bytes` (>= 1 MiB) of pinned host memory each way, one
+ * stream per direction, 64 MiB copies; *h2d and *d2h one direction alone,
+ * *both the total of the two directions copied at once; GB/s, best of `reps`.
+ * bench.py reports pcie_inclusive against it. */
+int cloudsc_pcie_gbps(int device, long long bytes, int reps, double *h2d, double *d2h, double *both);
 
 /* ABI introspection for bindings: sizeof of the public structs
  * (0 params, 1 fields, 2 template, 3 reference, 4 stats), -1 otherwise. */
@@ -381,18 +388,22 @@ typedef struct cloudsc_host_pipeline cloudsc_host_pipeline_t;
 
 /* `host` holds HOST pointers in block layout (full NPROMA blocks, the
  * precision's element type, ktype int).  The arrays are pinned in place
- * (hipHostRegister) until destroy; device buffers for `nstreams` chunks of
- * `chunk_blocks` blocks are allocated here.  cloudsc_gpu_init must have been
- * called for the device; the pipeline keeps a copy of the device's default
- * parameter set as it is at creation. */
+ * (hipHostRegister) until destroy; device buffers for `nstreams` chunk slots of
+ * `chunk_blocks` blocks each are allocated here (1..16; chunk c uses slot
+ * c % nstreams).  cloudsc_gpu_init must have been called for the device; the
+ * pipeline keeps a copy of the device's default parameter set as it is at
+ * creation. */
 int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t **pipe, int device, int precision, int ngptot,
                                  int nproma, int klev, int chunk_blocks, int nstreams,
                                  const cloudsc_fields_t *host);
 
-/* One step over all columns: per chunk H2D(inputs, plude) -> kernel -> D2H
- * (outputs, plude) on stream chunk % nstreams.  *ms = elapsed time of the
- * whole pipeline (transfers included), HIP events on the null stream.
- * KSEG: CLOUDSC_EHANDOFF if a segment hand-off timed out in any chunk. */
+/* One step over all columns, pipelined over three streams: every H2D copy
+ * (inputs, plude) on one, every kernel on a second, every D2H copy (outputs,
+ * plude) on a third, ordered per chunk slot by events, so chunk c's inputs
+ * move in while chunk c-1 computes and chunk c-2's outputs move out.  *ms =
+ * elapsed time of the whole pipeline (transfers included), HIP events on the
+ * null stream.  KSEG: CLOUDSC_EHANDOFF if a segment hand-off timed out in any
+ * chunk. */
 int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t *pipe, int variant, double *ms);
 
 int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t *pipe);

@@ -84,14 +84,14 @@ def test_gpu_lib_fails_loudly_without_library(tmp_path, monkeypatch):
 
 def test_state_layout_knob_arguments(lib):
     """The diagnostic placement knob accepts staggers that keep every field
-    aligned (multiples of 256 bytes; -1 = the default) and allocation flags
-    (hipExtMallocWithFlags; admitted again in round 4, the round-3 wrong values
-    were an unordered parameter upload: profiles/r04/contiguous_alloc_hazard.txt).
-    Misaligned staggers are refused.  No device call."""
+    aligned (multiples of 256 bytes; -1 = the default) and refuses misaligned
+    ones and hipExtMallocWithFlags flags: after destroyed states whose fields
+    were hipDeviceMallocContiguous allocations, later states computed wrong
+    values (profiles/r04/contiguous_alloc_hazard.txt).  No device call."""
     lib.cloudsc_debug_set_state_layout.argtypes = [C.c_longlong, C.c_uint]
     assert lib.cloudsc_debug_set_state_layout(100, 0) == ca.EINVAL
-    assert lib.cloudsc_debug_set_state_layout(4100, 4) == ca.EINVAL
-    assert lib.cloudsc_debug_set_state_layout(-1, 4) == 0
+    assert lib.cloudsc_debug_set_state_layout(-1, 4) == ca.EINVAL
+    assert lib.cloudsc_debug_set_state_layout(-1, 1) == ca.EINVAL
     assert lib.cloudsc_debug_set_state_layout(4608, 0) == 0
     assert lib.cloudsc_debug_set_state_layout((1 << 40) + 256, 0) == 0    # taken modulo 2 MiB
     assert lib.cloudsc_debug_set_state_layout(-1, 0) == 0

@@ -6,9 +6,10 @@
 // columns, NPROMA 64, KLEV 137 (28 input fields, 21 outputs, a KSEG workspace;
 // level / half-level / species / surface sizes, element size 8 or 4): every
 // field is allocated (hipMalloc, or hipExtMallocWithFlags(hipDeviceMallocContiguous)),
-// filled the way the state fills it -- inputs through a temporary hipMalloc'd
-// staging buffer (H2D copy from pageable memory, a copy kernel, hipFree of the
-// temporary), outputs by hipMemsetAsync -- all on one non-blocking stream, then
+// filled the way the state fills it -- inputs from a small template (the
+// 100-column reference state's size) copied into a temporary hipMalloc'd buffer
+// from pageable memory and expanded by a kernel, the temporary freed; outputs by
+// hipMemsetAsync -- all on one non-blocking stream, then
 // EVERY field is read back and checked (a field whose pages alias another's
 // shows the other's pattern), then everything is freed.  The sequence of states
 // is the one of profiles/r04/contiguous_alloc_hazard_repro.py --fp64-first:
@@ -34,6 +35,15 @@
 __global__ void copy_words(unsigned* dst, const unsigned* src, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     dst[i] = src[i];
+}
+// the state's expansion: dst[e] = src[(e / period) * klon + (e % period) % klon] for a small
+// template src of nrow x klon words (period = nproma columns; g % klon with no block offset
+// is enough to place every word)
+__global__ void expand_words(unsigned* dst, const unsigned* src, size_t n, int nproma, int klon, int nrow) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t row = (e / nproma) % nrow, col = (e / ((size_t)nproma * nrow) * nproma + e % nproma) % klon;
+    dst[e] = src[row * klon + col];
+  }
 }
 
 static unsigned pattern(int field, size_t i, unsigned salt) { return (unsigned)(i * 2654435761u) ^ (field * 0x9e3779b9u) ^ salt; }
@@ -70,14 +80,21 @@ int main(int argc, char** argv) {
       };
       std::vector<unsigned*> in(in_sz.size()), out(out_sz.size());
       std::vector<unsigned> h;
+      // inputs as the state expands them: a small template (nrow x 100 columns,
+      // 110-550 KB like the reference's 100-column state) copied in from pageable
+      // memory to a temporary, expanded by a kernel, the temporary freed
+      const int klon = 100;
+      std::vector<std::vector<unsigned>> tmpl(in_sz.size());
+      std::vector<int> nrow(in_sz.size());
       for (size_t f = 0; f < in_sz.size(); f++) {
         in[f] = dalloc(in_sz[f]);
-        h.resize(in_sz[f]);
-        for (size_t i = 0; i < h.size(); i++) h[i] = pattern((int)f, i, salt);
+        nrow[f] = (int)(in_sz[f] / ((size_t)nb * nproma));
+        tmpl[f].resize((size_t)nrow[f] * klon);
+        for (size_t i = 0; i < tmpl[f].size(); i++) tmpl[f][i] = pattern((int)f, i, salt);
         unsigned* tmp = nullptr;
-        CK(hipMalloc((void**)&tmp, in_sz[f] * 4));
-        CK(hipMemcpyAsync(tmp, h.data(), in_sz[f] * 4, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(copy_words, dim3(1024), dim3(256), 0, st, in[f], tmp, in_sz[f]);
+        CK(hipMalloc((void**)&tmp, tmpl[f].size() * 4));
+        CK(hipMemcpyAsync(tmp, tmpl[f].data(), tmpl[f].size() * 4, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(expand_words, dim3(1024), dim3(256), 0, st, in[f], tmp, in_sz[f], nproma, klon, nrow[f]);
         CK(hipGetLastError());
         CK(hipStreamSynchronize(st));
         CK(hipFree(tmp));
@@ -93,7 +110,10 @@ int main(int argc, char** argv) {
       for (size_t f = 0; f < in_sz.size(); f++) {
         h.resize(in_sz[f]);
         CK(hipMemcpy(h.data(), in[f], in_sz[f] * 4, hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < h.size(); i++) bad += h[i] != pattern((int)f, i, salt);
+        for (size_t e = 0; e < h.size(); e++) {
+          const size_t row = (e / nproma) % nrow[f], col = (e / ((size_t)nproma * nrow[f]) * nproma + e % nproma) % klon;
+          bad += h[e] != tmpl[f][row * klon + col];
+        }
       }
       for (size_t f = 0; f < out_sz.size(); f++) {
         h.resize(out_sz[f]);
