@@ -403,7 +403,8 @@ def gpu_lib(path: Optional[str] = None):
     lib.cloudsc_host_pipeline_destroy.argtypes = [C.c_void_p]
     lib.cloudsc_gpu_check.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
     lib.cloudsc_hbm_copy_gbps.argtypes = [C.c_int, C.c_longlong, C.c_int, C.POINTER(C.c_double)]
-    lib.cloudsc_pcie_gbps.argtypes = [C.c_int, C.c_longlong, C.c_int] + [C.POINTER(C.c_double)] * 3
+    if hasattr(lib, "cloudsc_pcie_gbps"):   # (older experiment builds lack it)
+        lib.cloudsc_pcie_gbps.argtypes = [C.c_int, C.c_longlong, C.c_int] + [C.POINTER(C.c_double)] * 3
     lib.cloudsc_cpu_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Params), C.POINTER(Fields),
                                     C.POINTER(C.c_double)]
     lib.cloudsc_debug_set_kseg_spin_limit.argtypes = [C.c_longlong]

@@ -558,6 +558,25 @@ template <typename real, typename P>
 CLOUDSC_HD real exp_liq(const P& c, real t) { return cl_exp<real>(c, cl_div_p<real>(c, c.r3les * (t - c.rtt), t - c.r4les)); }
 template <typename real, typename P>
 CLOUDSC_HD real exp_ice(const P& c, real t) { return cl_exp<real>(c, cl_div_p<real>(c, c.r3ies * (t - c.rtt), t - c.r4ies)); }
+// exp_liq and exp_ice of one temperature (the saturation values at T and in each
+// Newton step): the two divisions and exps are independent; in fp64 the exps
+// run as a pair with one range check (cloudsc_libm::exp_pair_split), so the
+// two chains interleave in one basic block (round 4, with the late range check
+// of exp_split: -1.3 % fp64 KSEG on the same box,
+// profiles/r04/experiment_exp_pair_ab.txt).  Same bits as the two calls.
+template <typename real, typename P>
+CLOUDSC_HD void exp_liq_ice(const P& c, real t, real& el, real& ei) {
+  const real ql = cl_div_p<real>(c, c.r3les * (t - c.rtt), t - c.r4les);
+  const real qi = cl_div_p<real>(c, c.r3ies * (t - c.rtt), t - c.r4ies);
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (std::is_same<real, double>::value) {
+    cloudsc_libm::exp_pair_split(ql, qi, &el, &ei, LdsLibmTabs{}, DevLibmCold{});
+    return;
+  }
+#endif
+  el = cl_exp<real>(c, ql);
+  ei = cl_exp<real>(c, qi);
+}
 
 // alfa*R5ALVCP/(T-R4LES)^2 + (1-alfa)*R5ALSCP/(T-R4IES)^2 (cloudsc_c.c:1166,1220)
 template <typename real, typename P>

@@ -292,10 +292,14 @@ int launch_kcache(hipStream_t st, const KArgs<real>& a, int nblocks, int nproma,
 // one-wave schedule that measures fastest (profiles/r01/nproma_sweep_*).
 int kseg_nsub(int nproma) { return (nproma + 63) / 64; }
 int kseg_wg(int nproma) { return nproma < 64 ? nproma : 64; }
-// workspace: [counter, err, pad..][flags: nblocks*nsub][carry state], 256-byte aligned parts
+// workspace: [err, tag, clock sums..][stripe counters, one per 128 B][flags: nblocks*nsub][carry state]
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr size_t kKsegCtrOffset = 256;                                   // bytes
+constexpr size_t kKsegFlagOffset = kKsegCtrOffset + kKsegStripes * kKsegCtrStride * sizeof(unsigned);
+static_assert(kKsegFlagOffset == 1280, "KSEG control layout");
+static_assert(sizeof(KsegEpoch::base) / sizeof(unsigned) == kKsegStripes, "one epoch base per stripe");
 size_t kseg_ctl_bytes(int nblocks, int nproma) {
-  return align256(256 + (size_t)nblocks * kseg_nsub(nproma) * sizeof(unsigned));
+  return align256(kKsegFlagOffset + (size_t)nblocks * kseg_nsub(nproma) * sizeof(unsigned));
 }
 template <typename real>
 size_t kseg_scratch_bytes(int nblocks, int nproma) {
@@ -334,6 +338,9 @@ void kseg_bounds(int nseg, int klev, int ncldtop, int split_pct, int* lev) {
   lev[nseg] = klev;
 }
 
+// dequeue stripes of a grid (cloudsc_kcache.h): one per XCD, never more than workgroups
+int kseg_nstripes(int grid) { return grid < kKsegStripes ? (grid > 0 ? grid : 1) : kKsegStripes; }
+
 // consumer spin bound of a KSEG hand-off (cloudsc_debug_set_kseg_spin_limit)
 std::atomic<unsigned> g_kseg_spin_limit{1u << 24};
 // schedule overrides for the tests of the hand-off (cloudsc_debug_set_kseg_schedule); 0 = default
@@ -341,10 +348,11 @@ std::atomic<int> g_kseg_nseg{0}, g_kseg_grid{0};
 
 }  // namespace
 
-// KSEG workspace words: [0] dequeue counter, [1] timed-out hand-offs (sticky:
-// accumulated over launches until cloudsc_gpu_check reads and clears it),
-// [2] a tag marking [1] as initialised, [32..35] two 64-bit clock sums
-// (PersistArgs::clk, accumulated like [1]), [64..] per-sub-block flags.  This
+// KSEG workspace words: [1] timed-out hand-offs (sticky: accumulated over
+// launches until cloudsc_gpu_check reads and clears it), [2] a tag marking [1]
+// as initialised, [32..35] two 64-bit clock sums (PersistArgs::clk, accumulated
+// like [1]), [64 + 32 s] the dequeue counter of stripe s, [320..] per-sub-block
+// flags.  This
 // kernel zeroes the counter and the flags before every launch of the low-level
 // entry points, and before the first launch on a state's workspace (later
 // launches of the state continue the counter and the flag stamps, KsegEpoch);
@@ -353,11 +361,9 @@ constexpr unsigned kKsegTag = 0xC105D5C1u;
 constexpr size_t kKsegClkOffset = 128;   // bytes: words [32..35]
 __global__ void __launch_bounds__(256) kseg_prepare_kernel(unsigned* ws, int nflags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) {
-    ws[0] = 0u;
-    if (ws[2] != kKsegTag) { ws[1] = 0u; ws[2] = kKsegTag; ws[32] = ws[33] = ws[34] = ws[35] = 0u; }
-  }
-  for (int j = i; j < nflags; j += gridDim.x * blockDim.x) ws[64 + j] = 0u;
+  if (i == 0 && ws[2] != kKsegTag) { ws[1] = 0u; ws[2] = kKsegTag; ws[32] = ws[33] = ws[34] = ws[35] = 0u; }
+  if (i < kKsegStripes) ws[kKsegCtrOffset / 4 + i * kKsegCtrStride] = 0u;
+  for (int j = i; j < nflags; j += gridDim.x * blockDim.x) ws[kKsegFlagOffset / 4 + j] = 0u;
 }
 
 namespace {
@@ -402,7 +408,9 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
   grid = env_int("CLOUDSC_KSEG_GRID", 0) > 0 ? env_int("CLOUDSC_KSEG_GRID", 0) : grid;
 #endif
   if (grid > nitems) grid = nitems;
-  launch_physics(kern, dim3(grid), dim3(wg), lds, st, ev, a, pa);
+  PersistArgs<real> pg = pa;
+  pg.nstripes = kseg_nstripes(grid);
+  launch_physics(kern, dim3(grid), dim3(wg), lds, st, ev, a, pg);
   *grid_out = grid;
   return CLOUDSC_OK;
 }
@@ -453,10 +461,10 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
   } else if (variant == CLOUDSC_VARIANT_KSEG) {
     if (!scratch) return CLOUDSC_EINVAL;
     PersistArgs<real> pa;
-    pa.counter = (unsigned*)scratch;
+    pa.ctr = (unsigned*)((char*)scratch + kKsegCtrOffset);
     pa.err = (unsigned*)scratch + 1;
     pa.clk = (unsigned long long*)((char*)scratch + kKsegClkOffset);
-    pa.flags = (unsigned*)((char*)scratch + 256);
+    pa.flags = (unsigned*)((char*)scratch + kKsegFlagOffset);
     pa.state = (real*)((char*)scratch + kseg_ctl_bytes(nblocks, nproma));
     pa.nsub = kseg_nsub(nproma);
     pa.spin_limit = g_kseg_spin_limit.load(std::memory_order_relaxed);
@@ -496,7 +504,7 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
       hipLaunchKernelGGL(kseg_prepare_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, (unsigned*)scratch, nflags);
       if (ep) ep->ready = false;
     }
-    pa.base = zero_ws ? 0u : ep->base;
+    for (int q = 0; q < kKsegStripes; q++) pa.base[q] = zero_ws ? 0u : ep->base[q];
     pa.stamp = zero_ws ? 0u : ep->stamp;
     int grid = 0;
     if constexpr (CLOUDSC_KEEP_KERNEL(real, true, true))
@@ -507,7 +515,13 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
     if (rc) return rc;
     HIPCHK(hipGetLastError());
     if (ep) {   // the next launch on this workspace continues where this one ends
-      ep->base = pa.base + (unsigned)pa.nitems + (unsigned)grid;
+      // stripe q took its items plus one past-the-end ticket per workgroup of it
+      const int S = kseg_nstripes(grid);
+      for (int q = 0; q < kKsegStripes; q++) {
+        const unsigned nbs = q < S ? (unsigned)((nblocks - q + S - 1) / S) : 0u;
+        const unsigned wgs = q < S ? (unsigned)((grid - q + S - 1) / S) : 0u;
+        ep->base[q] = pa.base[q] + (unsigned)pa.nseg * nbs * (unsigned)pa.nsub + wgs;
+      }
       ep->stamp = pa.stamp + (unsigned)(kMaxSeg + 1);
       ep->ready = true;
     }

@@ -41,7 +41,8 @@ bool fields_complete(const cloudsc_fields_t* f);
 // continue its ticket counter and flag stamps instead of zeroing it again.
 struct KsegEpoch {
   bool ready = false;       // false: zero the workspace before the next launch
-  unsigned base = 0, stamp = 0;
+  unsigned base[8] = {};    // per dequeue stripe (kKsegStripes, cloudsc_kcache.h)
+  unsigned stamp = 0;
 };
 // Start/stop events of one launch, recorded by the kernel's own dispatch
 // (hipExtLaunchKernelGGL) instead of separate event packets around it.

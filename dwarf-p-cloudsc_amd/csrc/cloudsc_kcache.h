@@ -378,8 +378,13 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
 
     const real pap_k = in.pap;
     // saturation values (:583-609)
-    const real e_liq = CLOUDSC_RUN(AB_SAT) ? exp_liq<real>(c, ztp1) : launder_vgpr(ztp1 * R(0.02));
-    const real e_ice = CLOUDSC_RUN(AB_SAT) ? exp_ice<real>(c, ztp1) : launder_vgpr(ztp1 * R(0.019));
+    real e_liq, e_ice;
+    if (CLOUDSC_RUN(AB_SAT)) {
+      exp_liq_ice<real>(c, ztp1, e_liq, e_ice);
+    } else {
+      e_liq = launder_vgpr(ztp1 * R(0.02));
+      e_ice = launder_vgpr(ztp1 * R(0.019));
+    }
     // divisors shared by several divisions (cl_recip: one reciprocal, same quotient bits)
     const Recip<real> r_pap = cl_recip_p<real>(c, pap_k);
     const real zfoeewmt = fmin(cl_div_p<real>(c, (c.r2es * (zfoealfa * e_liq + (R(1.0) - zfoealfa) * e_ice)), r_pap), R(0.5));
@@ -565,7 +570,9 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
   #pragma unroll
       for (int it = 0; it < 2; it++) {
         const real a = foealfa<real>(c, tt);
-        real zqsat = (c.r2es * (a * exp_liq<real>(c, tt) + (R(1.0) - a) * exp_ice<real>(c, tt))) * zqp;
+        real el, ei;
+        exp_liq_ice<real>(c, tt, el, ei);
+        real zqsat = (c.r2es * (a * el + (R(1.0) - a) * ei)) * zqp;
         zqsat = fmin(R(0.5), zqsat);
         const real zcor2 = cl_div_p<real>(c, R(1.0), (R(1.0) - c.retv * zqsat));
         zqsat = zqsat * zcor2;
@@ -1296,6 +1303,19 @@ __device__ __forceinline__ void cloudsc_kcache_body(cptr<KArgs<real>> ka, cptr<P
 // with NSEG segments the tail shrinks to a fraction of a segment.
 constexpr int kCarryN = 19;
 constexpr int kMaxSeg = 16;
+// Dequeue stripes (round 4): the items are split into kKsegStripes independent
+// queues -- stripe s holds every segment of the blocks b with b % nstripes == s,
+// in the same (segment, block, sub-block) order -- each with its own counter on
+// its own 128-byte line, and workgroup w takes its items from stripe
+// w % nstripes (the round-robin dispatch puts it on XCD w % 8).  At start-up
+// 2048 workgroups then queue on 8 counters instead of one (round 3: the last
+// first item began 23 us after the first).  Progress needs no residency: within
+// a stripe items are dequeued in order, so an item's predecessor (the same
+// block's previous segment, same stripe) was dequeued earlier by a running
+// workgroup.  A stripe's counter advances by exactly its items plus the
+// workgroups of the stripe per launch (each takes one ticket past the end).
+constexpr int kKsegStripes = 8;
+constexpr int kKsegCtrStride = 32;   // words between stripe counters (128 B)
 
 #ifdef CLOUDSC_KSEG_TRACE
 constexpr int kTraceMax = 1 << 16;
@@ -1309,10 +1329,13 @@ struct PersistArgs {
   // exactly nitems + grid tickets, so the host passes the counter's value at
   // its start (base), and flags are stamped per launch (stamp + segments done;
   // an older launch's flag compares as "not yet": signed difference).
-  unsigned* counter;      // dequeue counter: this launch's tickets are base, base + 1, ...
+  unsigned* ctr;          // stripe s's dequeue counter at ctr[s * kKsegCtrStride]: its tickets are
+                          // base[s], base[s] + 1, ...
   unsigned* flags;        // [nblocks * nsub] stamp + segments completed
   unsigned* err;          // spin-limit violations (sticky until read, cloudsc_gpu_check)
-  unsigned base, stamp;   // 0, 0 right after zeroing
+  unsigned base[kKsegStripes];   // 0 right after zeroing
+  unsigned stamp;         // 0 right after zeroing
+  int nstripes;           // 1..kKsegStripes, <= grid
   real* state;            // [nblocks][kCarryN][nproma]
   int nseg, nitems, nblocks;
   int nsub;               // 64-column sub-blocks per NPROMA block (one wave each)
@@ -1367,23 +1390,33 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
   const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;
   const unsigned one = threadIdx.x == 0 ? 1u : 0u;  // lane 0 counts, the others add 0
   const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+  // this workgroup's stripe: blocks b = lb * S + st, lb < nbs (all wave-uniform)
+  const int S = P.nstripes;
+  const int st = (int)(blockIdx.x % (unsigned)S);
+  const int nbs = (P.nblocks - st + S - 1) / S;
+  const int nsbs = nbs * nsub;                        // items per segment in the stripe
+  const int items = P.nseg * nsbs;
+  unsigned* const ctr = P.ctr + st * kKsegCtrStride;
+  const unsigned base = P.base[st];
   for (;;) {
     if (wave0) {
-      const unsigned old = __hip_atomic_fetch_add(P.counter, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_item = (int)(__builtin_amdgcn_readfirstlane(old) - P.base);   // lane 0's value: the ticket
+      const unsigned old = __hip_atomic_fetch_add(ctr, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_item = (int)(__builtin_amdgcn_readfirstlane(old) - base);   // lane 0's value: the ticket
     }
     __syncthreads();
     const int item = __builtin_amdgcn_readfirstlane(s_item);
     __syncthreads();                                   // s_item is rewritten next iteration
-    if (item >= P.nitems) break;
-    // item = (segment, block b, 64-column sub-block h), segment-major (or
-    // (segment, h, b) with sb_major): a block of NPROMA > 64 columns is run
+    if (item >= items) break;
+    // item = (segment, stripe block lb, 64-column sub-block h), segment-major
+    // (or (segment, h, lb) with sb_major): a block of NPROMA > 64 columns is run
     // as nsub one-wave items over the same block layout (sub-block h is the 64
     // contiguous columns h*64.. of each plane); flags are per (b, h)
-    const int nsb = P.nblocks * nsub;
-    const int seg = item / nsb, sb = item - seg * nsb;
-    const int b = P.sb_major ? sb % P.nblocks : sb / nsub;
-    const int jl = (P.sb_major ? sb / P.nblocks : sb - b * nsub) * 64 + (int)threadIdx.x;
+    const int seg = item / nsbs, r = item - seg * nsbs;
+    const int lb = P.sb_major ? r % nbs : r / nsub;
+    const int hh = P.sb_major ? r / nbs : r - lb * nsub;
+    const int b = lb * S + st;
+    const int sb = b * nsub + hh;
+    const int jl = hh * 64 + (int)threadIdx.x;
     const unsigned lo = (unsigned)jl * (unsigned)sizeof(real);
 #ifdef CLOUDSC_KSEG_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -1433,11 +1466,12 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
       stg(((const KArgs<real>*)launder_uniform(ka))->prainfrac, (size_t)b * nproma, lo, cs.rainfrac);
     }
 #ifdef CLOUDSC_KSEG_TRACE
-    if (threadIdx.x == 0 && item < kTraceMax) {   // diagnostic build only: schedule of every item
-      g_kseg_trace[4 * item + 0] = t_start;
-      g_kseg_trace[4 * item + 1] = __builtin_amdgcn_s_memrealtime();
-      g_kseg_trace[4 * item + 2] = blockIdx.x;
-      g_kseg_trace[4 * item + 3] = t_ready;
+    const int gitem = seg * P.nblocks * nsub + sb;   // the item's index in the unstriped order
+    if (threadIdx.x == 0 && gitem < kTraceMax) {   // diagnostic build only: schedule of every item
+      g_kseg_trace[4 * gitem + 0] = t_start;
+      g_kseg_trace[4 * gitem + 1] = __builtin_amdgcn_s_memrealtime();
+      g_kseg_trace[4 * gitem + 2] = blockIdx.x;
+      g_kseg_trace[4 * gitem + 3] = t_ready;
     }
 #endif
   }

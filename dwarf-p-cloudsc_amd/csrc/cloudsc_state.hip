@@ -39,7 +39,8 @@ __global__ void expand_kernel(T* __restrict__ dst, const S* __restrict__ src, in
 // Double-double accumulation of non-negative terms (Knuth's TwoSum, then a
 // renormalisation): hi + lo carries the sum to ~100 bits, so partial sums
 // combined in any grouping -- NPROMA blocks here, shards or ranks on the host --
-// round to the same double.  No FMA contraction applies (-ffp-contract=off),
+// round to the same double unless the exact sum lies within ~2^-100 of a
+// rounding midpoint.  No FMA contraction applies (-ffp-contract=off),
 // and nothing here is reassociated (no fast-math).
 struct DD {
   double hi, lo;
@@ -453,7 +454,7 @@ int cloudsc_state_validate(cloudsc_gpu_state_t* s, const cloudsc_reference_t* re
     if (e == hipSuccess) e = hipMemcpy(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost);
     if (e != hipSuccess) break;
     cloudsc_stats_t t = {__DBL_MAX__, -__DBL_MAX__, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int b = 0; b < s->nblocks; b++) {            // double-double sums: any order gives the same double
+    for (int b = 0; b < s->nblocks; b++) {            // double-double sums: order-independent to ~2^-100
       const double* q = &h[(size_t)b * kStatsPer];
       const cloudsc_stats_t pb = {q[0], q[1], q[2], q[3], q[4], q[5], q[6]};
       cloudsc_stats_combine(&t, &pb);

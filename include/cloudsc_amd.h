@@ -313,9 +313,11 @@ typedef struct cloudsc_reference {
  * rounded to double, errsum_lo / refsum_lo what that rounding left over (all
  * terms are non-negative, so hi + lo holds the sum to ~100 bits).  Sums of
  * partial statistics -- NPROMA blocks on the device, shards on the host, the
- * MPI_Reduce of validate_mod.F90:53-55 -- therefore do not depend on how the
- * columns were partitioned: a sharded run prints the unsharded run's table to
- * the last digit.  Combine partials with cloudsc_stats_combine. */
+ * MPI_Reduce of validate_mod.F90:53-55 -- therefore depend on how the columns
+ * were partitioned only within the double-double error (~2^-100 relative): in
+ * practice a sharded run prints the unsharded run's table to the last digit; a
+ * total within that distance of a rounding midpoint could round 1 ulp apart.
+ * Combine partials with cloudsc_stats_combine. */
 typedef struct cloudsc_stats {
   double minval, maxval, maxerr, errsum, refsum;
   double errsum_lo, refsum_lo;

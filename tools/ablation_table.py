@@ -11,6 +11,7 @@ import re
 import sys
 
 d0 = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/abl"
+P = "F32" if len(sys.argv) > 2 and sys.argv[2] == "fp32" else "F64"
 times = {}
 for line in open(os.path.join(d0, "times.txt")):
     m = re.match(r"(\S+)\.so\s+median ([\d.]+) ms.*ratio-to-first ([\d.]+)", line)
@@ -39,12 +40,12 @@ for d in sorted(glob.glob(os.path.join(d0, "pmc_*/"))):
     rows[n] = (cnt, ms)
 base = rows["full"][0]["SQ_INSTS_VALU"]
 order = sorted(rows, key=lambda n: times.get(n, (0, 9))[1])
-print("%-9s %10s %8s %8s %9s %9s %9s %9s %8s %7s" % ("build", "time ms", "t/full", "VALU", "dVALU %", "FMA64",
-                                                    "MUL64", "ADD64", "pmc ms", "GHz"))
+print("%-9s %10s %8s %8s %9s %9s %9s %9s %8s %7s" % ("build", "time ms", "t/full", "VALU", "dVALU %", "FMA",
+                                                    "MUL", "ADD", "pmc ms", "GHz"))
 for n in order:
     c, ms = rows[n]
     t = times.get(n, (float("nan"), float("nan")))
     ghz = c["GRBM_GUI_ACTIVE"] / 8 / (ms * 1e-3) / 1e9
     print("%-9s %10.4f %8.4f %8.3e %9.1f %9.3e %9.3e %9.3e %8.3f %7.2f" % (
-        n, t[0], t[1], c["SQ_INSTS_VALU"], 100 * (c["SQ_INSTS_VALU"] / base - 1), c["SQ_INSTS_VALU_FMA_F64"],
-        c["SQ_INSTS_VALU_MUL_F64"], c["SQ_INSTS_VALU_ADD_F64"], ms, ghz))
+        n, t[0], t[1], c["SQ_INSTS_VALU"], 100 * (c["SQ_INSTS_VALU"] / base - 1), c["SQ_INSTS_VALU_FMA_" + P],
+        c["SQ_INSTS_VALU_MUL_" + P], c["SQ_INSTS_VALU_ADD_" + P], ms, ghz))
