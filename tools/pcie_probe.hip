@@ -69,6 +69,26 @@ double run_blit(const Bufs& b, int dir, int grid, std::vector<hipStream_t>& st) 
   return now() - t0;
 }
 
+// both directions at once, one by the copy engine and one by a blit kernel
+// (h2d_blit: H2D blit + D2H sdma; else H2D sdma + D2H blit), 64 MiB copies
+double run_mixed(const Bufs& b, bool h2d_blit, int grid, std::vector<hipStream_t>& st) {
+  CK(hipDeviceSynchronize());
+  const double t0 = now();
+  const size_t n = b.bytes / sizeof(v4u), piece = (size_t)64 << 20;
+  if (h2d_blit) {
+    hipLaunchKernelGGL(blit, dim3(grid), dim3(256), 0, st[0], (v4u*)b.d_in, (const v4u*)b.h_in, n);
+    for (size_t off = 0; off < b.bytes; off += piece)
+      CK(hipMemcpyAsync(b.h_out + off, b.d_out + off, std::min(piece, b.bytes - off), hipMemcpyDeviceToHost, st[1]));
+  } else {
+    for (size_t off = 0; off < b.bytes; off += piece)
+      CK(hipMemcpyAsync(b.d_in + off, b.h_in + off, std::min(piece, b.bytes - off), hipMemcpyHostToDevice, st[0]));
+    hipLaunchKernelGGL(blit, dim3(grid), dim3(256), 0, st[1], (v4u*)b.h_out, (const v4u*)b.d_out, n);
+  }
+  CK(hipGetLastError());
+  CK(hipDeviceSynchronize());
+  return now() - t0;
+}
+
 int main(int argc, char** argv) {
   const double gib = argc > 1 ? atof(argv[1]) : 2.0;
   Bufs b;
@@ -107,6 +127,16 @@ int main(int argc, char** argv) {
                   grid, gbs);
       std::fflush(stdout);
     }
+  }
+  // repeatability of the both-direction forms: 10 runs each, every time printed
+  for (int mode = 0; mode < 3; mode++) {
+    std::printf("{\"repeat\": \"%s\", \"GBs_total\": [", mode == 0 ? "sdma+sdma" : mode == 1 ? "sdma_h2d+blit_d2h" : "blit_h2d+sdma_d2h");
+    for (int r = 0; r < 10; r++) {
+      const double t = mode == 0 ? run_sdma(b, 3, 1, (size_t)64 << 20, st) : run_mixed(b, mode == 2, 256, st);
+      std::printf("%s%.1f", r ? ", " : "", 2.0 * b.bytes / t / 1e9);
+    }
+    std::printf("]}\n");
+    std::fflush(stdout);
   }
   std::printf("{\"summary\": true, \"bytes_each_direction\": %zu, \"sdma_h2d\": %.1f, \"sdma_d2h\": %.1f, "
               "\"sdma_both_total\": %.1f, \"blit_h2d\": %.1f, \"blit_d2h\": %.1f, \"blit_both_total\": %.1f}\n",

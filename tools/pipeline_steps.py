@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Diagnostic: step-to-step spread of the host-buffer pipeline
+(cloudsc_host_pipeline_run) -- every step's time, for host arrays from numpy
+(pinned in place by the pipeline with hipHostRegister) and for the same arrays
+in hipHostMalloc memory (already pinned; the pipeline uses them as they are).
+usage: pipeline_steps.py [steps] [chunk_blocks] [slots]"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "dwarf-p-cloudsc_amd"))
+import cloudsc_amd as ca  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 15
+chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+slots = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+ds = ca.load_dataset()
+hip = C.CDLL("libamdhip64.so")
+hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+hip.hipHostFree.argtypes = [C.c_void_p]
+
+
+def run(kind):
+    hp = ca.HostPipeline.__new__(ca.HostPipeline)
+    if kind == "registered":
+        hp = ca.HostPipeline(ds, 163840, 64, ca.FP64, chunk_blocks=chunk, nstreams=slots)
+        keep = []
+    else:
+        # the same state, every array moved into hipHostMalloc memory before the pipeline is created
+        lib = ca.gpu_lib()
+        params = ca.Params.from_dict(ds.params)
+        ca.check(lib.cloudsc_gpu_init(0, C.byref(params)))
+        st = ca.make_host_state(ds, 163840, 64, ca.FP64)
+        keep = []
+        for name, a in list(st.arrays.items()):
+            p = C.c_void_p()
+            assert hip.hipHostMalloc(C.byref(p), a.nbytes, 0) == 0
+            keep.append(p)
+            v = np.ctypeslib.as_array((C.c_byte * a.nbytes).from_address(p.value)).view(a.dtype).reshape(a.shape)
+            v[...] = a
+            st.arrays[name] = v
+        hp.lib, hp.ds, hp.ngptot, hp.nproma, hp.precision = lib, ds, 163840, 64, ca.FP64
+        hp._params, hp.state, hp._plude0 = params, st, st.arrays["plude"].copy()
+        f = st.fields()
+        for name in ca.AEROSOL_FIELDS:
+            setattr(f, name, None)
+        hp._fields = f
+        h = C.c_void_p()
+        ca.check(lib.cloudsc_host_pipeline_create(C.byref(h), 0, ca.FP64, 163840, 64, ds.klev, chunk, slots,
+                                                  C.byref(f)))
+        hp.h = h
+    try:
+        hp.run(ca.VARIANT_KSEG)
+        ms = [round(hp.run(ca.VARIANT_KSEG), 2) for _ in range(steps)]
+    finally:
+        hp.close()
+        for p in keep:
+            hip.hipHostFree(p)
+    print(json.dumps({"host_memory": kind, "chunk_blocks": chunk, "slots": slots, "ms": ms,
+                      "median": float(np.median(ms)), "min": min(ms)}), flush=True)
+
+
+for kind in ("registered", "hostmalloc", "registered"):
+    run(kind)
