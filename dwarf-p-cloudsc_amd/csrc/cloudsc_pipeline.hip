@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
@@ -78,6 +79,37 @@ size_t per_block_elems(int kind, int nproma, int klev) {
 
 }  // namespace
 
+// D2H of one chunk by a copy kernel instead of the copy engine (diagnostic
+// mode, cloudsc_debug_set_pipeline_d2h_blit): every output field's chunk range,
+// device buffer -> pinned host memory through its device-visible address, in
+// one launch.  16-byte accesses where both ends are 16-byte aligned, else 4 B.
+constexpr int kMaxBlitSeg = 24;
+struct BlitSegs {
+  const char* src[kMaxBlitSeg];
+  char* dst[kMaxBlitSeg];
+  unsigned long long bytes[kMaxBlitSeg];
+  int n;
+};
+__global__ void __launch_bounds__(256) d2h_blit_kernel(const BlitSegs s) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+  for (int q = 0; q < s.n; q++) {
+    const char* src = s.src[q];
+    char* dst = s.dst[q];
+    const size_t nb = s.bytes[q];
+    if ((((uintptr_t)src | (uintptr_t)dst | nb) & 15) == 0) {
+      const u4* a = (const u4*)src;
+      u4* b = (u4*)dst;
+      for (size_t i = tid; i < nb / 16; i += nth) __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+    } else {
+      const unsigned* a = (const unsigned*)src;
+      unsigned* b = (unsigned*)dst;
+      for (size_t i = tid; i < nb / 4; i += nth) __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+    }
+  }
+}
+std::atomic<int> g_pipe_d2h_blit{0};
+
 struct cloudsc_host_pipeline {
   int device, precision, ngptot, nproma, klev, nblocks, chunk_blocks, nstreams;   // nstreams: device slots
   size_t es;
@@ -92,6 +124,7 @@ struct cloudsc_host_pipeline {
   };
   std::vector<Slot> slots;
   hipStream_t st_in = nullptr, st_k = nullptr, st_out = nullptr;
+  void* host_dev[kNumFields] = {};   // device-visible addresses of the pinned host arrays (D2H by blit kernel)
   std::vector<void*> allocs;
   ParamSet params;          // snapshot of the device's default set at creation
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -142,15 +175,20 @@ int pin_host_fields(cloudsc_host_pipeline* p, void* const* hf) {
     const hipError_t e = hipHostRegister((void*)s.lo, s.hi - s.lo, hipHostRegisterDefault);
     if (e == hipSuccess) { p->pinned.push_back((void*)s.lo); continue; }
     (void)hipGetLastError();
-    if (e != hipErrorHostMemoryAlreadyRegistered) return hip_fail(e, "hipHostRegister");
+    // memory pinned by the caller: hipHostRegister reports it as already
+    // registered, or (hipHostMalloc memory, ROCm 7) as an invalid argument
+    bool all_pinned = true, any_pinned = false;
     for (int i = 0; i < kNumFields; i++) {
       const uintptr_t a = (uintptr_t)hf[i];
       if (!hf[i] || a < s.lo || a >= s.hi) continue;
-      if (!pinned_as_one(hf[i], field_bytes(p, i, p->nblocks))) {
-        set_error_text("host pipeline: an array lies partly in memory pinned by the caller; pin all or none");
-        return CLOUDSC_EINVAL;
-      }
+      const bool one = pinned_as_one(hf[i], field_bytes(p, i, p->nblocks));
+      all_pinned = all_pinned && one;
+      any_pinned = any_pinned || one;
     }
+    if (all_pinned) continue;
+    if (e != hipErrorHostMemoryAlreadyRegistered && !any_pinned) return hip_fail(e, "hipHostRegister");
+    set_error_text("host pipeline: an array lies partly in memory pinned by the caller; pin all or none");
+    return CLOUDSC_EINVAL;
   }
   return CLOUDSC_OK;
 }
@@ -182,6 +220,12 @@ int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int 
   if ((rc = param_set_copy(&p->params, device_default_params(device)))) return fail(rc);
   void* const* hf = (void* const*)&p->host;
   if ((rc = pin_host_fields(p, hf))) return fail(rc);
+  for (int i = 0; i < kNumFields; i++) {   // device-visible addresses of the pinned arrays (D2H blit mode)
+    if (!hf[i]) continue;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, hf[i], 0) == hipSuccess) p->host_dev[i] = d;
+    else (void)hipGetLastError();
+  }
   for (hipStream_t* q : {&p->st_in, &p->st_k, &p->st_out})
     if (hipStreamCreateWithFlags(q, hipStreamNonBlocking) != hipSuccess) return fail(CLOUDSC_EHIP);
   // more slots than chunks would never be used
@@ -264,12 +308,25 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
     HIPCHK(hipEventRecord(s.k_done, p->st_k));
     // outputs (and plude): after the kernel
     HIPCHK(hipStreamWaitEvent(p->st_out, s.k_done, 0));
+    BlitSegs bs{};
+    bool blit = g_pipe_d2h_blit.load(std::memory_order_relaxed) != 0;
     for (int i = 0; i < kNumFields; i++) {
       const FieldDesc& d = kFieldTable[i];
       if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
       const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * p->es;
+      if (blit && p->host_dev[i] && bs.n < kMaxBlitSeg) {
+        bs.src[bs.n] = (const char*)df[i];
+        bs.dst[bs.n] = (char*)p->host_dev[i] + (size_t)b0 * per;
+        bs.bytes[bs.n] = (unsigned long long)((size_t)nb * per);
+        bs.n++;
+        continue;
+      }
       HIPCHK(hipMemcpyAsync((char*)hf[i] + (size_t)b0 * per, df[i], (size_t)nb * per, hipMemcpyDeviceToHost,
                             p->st_out));
+    }
+    if (bs.n) {
+      hipLaunchKernelGGL(d2h_blit_kernel, dim3(256), dim3(256), 0, p->st_out, bs);
+      HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(s.out_done, p->st_out));
   }
@@ -327,6 +384,11 @@ int cloudsc_debug_host_pipeline_mapping(const cloudsc_host_pipeline_t* p, int* n
   }
   *n_arrays = n;
   *n_not_one_mapping = bad;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_debug_set_pipeline_d2h_blit(int on) {
+  g_pipe_d2h_blit.store(on ? 1 : 0, std::memory_order_relaxed);
   return CLOUDSC_OK;
 }
 

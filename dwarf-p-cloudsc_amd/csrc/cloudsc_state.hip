@@ -112,6 +112,7 @@ struct cloudsc_gpu_state {
   cloudsc_impl::KsegEpoch kseg_epoch;   // where the last launch on kseg_ws left its counter and flag stamps
   ParamSet params;                // the state's own parameter set (never shared)
   std::vector<void*> allocs;
+  size_t fbytes[sizeof(cloudsc_fields_t) / sizeof(void*)];   // bytes of each field, cloudsc_fields_t order
 };
 
 namespace {
@@ -276,16 +277,23 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
     if ((rc = dalloc(s, &base, total))) return fail(rc);
     ar.base = (char*)base;
   }
+  std::memset(s->fbytes, 0, sizeof(s->fbytes));
+  auto member = [&](const void* slot) {
+    const ptrdiff_t m = (const void* const*)slot - (const void* const*)&s->f;
+    return m >= 0 && m < (ptrdiff_t)(sizeof(s->fbytes) / sizeof(s->fbytes[0])) ? (int)m : -1;
+  };
   for (In& in : ins) {
     if (!in.src) continue;
     void* p = nullptr;
     if ((rc = field_alloc(s, ar, &p, in.bytes))) return fail(rc);
     if ((rc = expand_into(s, p, in.src, in.nlev, in.is_int))) return fail(rc);
     *in.dst = p;
+    if (member(in.dst) >= 0) s->fbytes[member(in.dst)] = in.bytes;
   }
   s->plude_pristine = plude_dev;
   for (Out& o : outs) {
     if ((rc = field_alloc(s, ar, o.dst, o.bytes))) return fail(rc);
+    if (member(o.dst) >= 0) s->fbytes[member(o.dst)] = o.bytes;
     if (hipMemsetAsync(*o.dst, 0xff, o.bytes, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);  // NaN
   }
   if (hipMemcpyAsync(f.plude, s->plude_pristine, n2, hipMemcpyDeviceToDevice, s->stream) != hipSuccess)
@@ -318,6 +326,24 @@ int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags) {
   if (alloc_flags != 0) return CLOUDSC_EINVAL;
 #endif
   g_layout_stagger.store(stagger < 0 ? -1 : stagger % (long long)kArenaAlign);
+  return CLOUDSC_OK;
+}
+
+int cloudsc_debug_state_relocate_field(cloudsc_gpu_state_t* s, int member) {
+  const int nmem = (int)(sizeof(s->fbytes) / sizeof(s->fbytes[0]));
+  if (!s || member < 0 || member >= nmem) return CLOUDSC_EINVAL;
+  void** slot = (void**)&s->f + member;
+  const size_t bytes = s->fbytes[member];
+  if (!*slot || !bytes) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(s->device));
+  // the old allocation stays with the state until it is destroyed, so the copy
+  // lands on other physical pages
+  void* q = nullptr;
+  int rc = dalloc(s, &q, bytes);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(q, *slot, bytes, hipMemcpyDeviceToDevice, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  *slot = q;
   return CLOUDSC_OK;
 }
 

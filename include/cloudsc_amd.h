@@ -342,6 +342,14 @@ int cloudsc_state_create(cloudsc_gpu_state_t **state, int device, int precision,
  * default parameter set, not the state's). */
 int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out);
 
+/* Diagnostic: move field `member` (its position in cloudsc_fields_t) of a state
+ * to a new device allocation, contents copied; the old allocation is kept until
+ * the state is destroyed, so the field lands on other physical pages.  For
+ * finding which fields' placement decides the kernel time
+ * (tools/placement_fields.py).  CLOUDSC_EINVAL for a member the state does not
+ * hold (aerosol fields it was created without). */
+int cloudsc_debug_state_relocate_field(cloudsc_gpu_state_t *s, int member);
+
 /* Restore plude from the pristine copy -- for callers that run in place
  * through cloudsc_gpu_run on the state's buffers. */
 int cloudsc_state_reset(cloudsc_gpu_state_t *state);
@@ -423,6 +431,12 @@ int cloudsc_debug_host_pipeline_mapping(const cloudsc_host_pipeline_t *pipe, int
  * by the device as one mapping, 0 if not (e.g. after the pipeline that pinned
  * it was destroyed). */
 int cloudsc_debug_host_pinned(const void *ptr, long long bytes);
+
+/* Diagnostic: host pipelines run after this call copy their outputs back with
+ * a copy kernel writing the pinned host memory through its device-visible
+ * address (on = 1) instead of the copy engine (0, the default); for measuring
+ * the two directions' overlap (tools/pipeline_steps.py). */
+int cloudsc_debug_set_pipeline_d2h_blit(int on);
 
 /* ------------------------------------------------------------------------ */
 /* One synchronous step on host arrays, callable from any host thread        */

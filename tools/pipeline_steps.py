@@ -2,8 +2,11 @@
 """Diagnostic: step-to-step spread of the host-buffer pipeline
 (cloudsc_host_pipeline_run) -- every step's time, for host arrays from numpy
 (pinned in place by the pipeline with hipHostRegister) and for the same arrays
-in hipHostMalloc memory (already pinned; the pipeline uses them as they are).
-usage: pipeline_steps.py [steps] [chunk_blocks] [slots]"""
+in hipHostMalloc memory (already pinned; the pipeline uses them as they are),
+with the outputs copied back by the copy engine or by a copy kernel
+(cloudsc_debug_set_pipeline_d2h_blit).
+usage: pipeline_steps.py [steps] [chunk_blocks] [slots] [modes]
+modes: comma-separated of reg, reg-blit, hm, hm-blit (default: all, then reg again)"""
 import ctypes as C
 import json
 import os
@@ -24,7 +27,8 @@ hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
 hip.hipHostFree.argtypes = [C.c_void_p]
 
 
-def run(kind):
+def run(kind, blit=0):
+    ca.gpu_lib().cloudsc_debug_set_pipeline_d2h_blit(blit)
     hp = ca.HostPipeline.__new__(ca.HostPipeline)
     if kind == "registered":
         hp = ca.HostPipeline(ds, 163840, 64, ca.FP64, chunk_blocks=chunk, nstreams=slots)
@@ -60,9 +64,14 @@ def run(kind):
         hp.close()
         for p in keep:
             hip.hipHostFree(p)
-    print(json.dumps({"host_memory": kind, "chunk_blocks": chunk, "slots": slots, "ms": ms,
+    print(json.dumps({"host_memory": kind, "d2h": "blit kernel" if blit else "copy engine",
+                      "chunk_blocks": chunk, "slots": slots, "ms": ms,
                       "median": float(np.median(ms)), "min": min(ms)}), flush=True)
 
 
-for kind in ("registered", "hostmalloc", "registered"):
-    run(kind)
+MODES = {"reg": ("registered", 0), "reg-blit": ("registered", 1), "hm": ("hostmalloc", 0),
+         "hm-blit": ("hostmalloc", 1)}
+modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["reg", "reg-blit", "hm", "hm-blit", "reg"]
+for m in modes:
+    run(*MODES[m])
+ca.gpu_lib().cloudsc_debug_set_pipeline_d2h_blit(0)
