@@ -233,7 +233,8 @@ def main():
             "kernel_ms": round(float(np.mean(kernel_ms)), 4), "kernel_ms_min": round(float(np.min(kernel_ms)), 4),
             "kernel_ms_median": round(float(np.median(kernel_ms)), 4),
             "stream_gbs": round(peak_meas, 1) if peak_meas else None,
-            "sclk_ghz": round(sclk, 4) if sclk else None, "prewarm_steps": prewarm}
+            "sclk_ghz": round(sclk, 4) if sclk else None, "prewarm_steps": prewarm,
+            "placement": g.placement()}
     per_rank = ctl.gather_records(mine)
 
     # validation of the last step against reference.h5 (device-side statistics, combined over ranks)
@@ -288,6 +289,9 @@ def main():
         "sclk_ghz": round(sclk, 4) if sclk else None,
         "sclk_method": "effective shader clock of the timed launches: each workgroup's s_memtime cycles over its "
                        "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",
+        "placement": dict(per_rank[0]["placement"], method=(
+            "output placement search at state creation (cloudsc_state_placement): a write-only kernel with the "
+            "physics kernel's output pattern timed before / after moving output fields to fresh allocations; rank 0")),
         "per_rank": per_rank,
         "validation_worst_rel_l1": worst,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

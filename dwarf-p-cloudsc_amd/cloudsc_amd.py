@@ -394,6 +394,14 @@ def gpu_lib(path: Optional[str] = None):
     lib.cloudsc_state_sync.argtypes = [C.c_void_p]
     lib.cloudsc_state_reset.argtypes = [C.c_void_p]
     lib.cloudsc_state_fields.argtypes = [C.c_void_p, C.POINTER(Fields)]
+    if hasattr(lib, "cloudsc_state_placement"):
+        lib.cloudsc_state_placement.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                                C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        lib.cloudsc_debug_set_placement_search.argtypes = [C.c_int]
+    if hasattr(lib, "cloudsc_debug_set_pipeline_copy"):
+        lib.cloudsc_debug_set_pipeline_copy.argtypes = [C.c_int]
+        lib.cloudsc_debug_host_pipeline_copy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                                         C.POINTER(C.c_int)]
     lib.cloudsc_gpu_init.argtypes = [C.c_int, C.POINTER(Params)]
     lib.cloudsc_gpu_run.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.POINTER(Fields), C.c_void_p]
@@ -573,6 +581,13 @@ class GpuState:
         check(self.lib.cloudsc_state_kseg_clock(self.h, int(reset), C.byref(ghz)))
         return ghz.value
 
+    def placement(self) -> dict:
+        """The output placement search of this state (cloudsc_state_placement)."""
+        a, b, t, m = C.c_float(), C.c_float(), C.c_int(), C.c_int()
+        check(self.lib.cloudsc_state_placement(self.h, C.byref(a), C.byref(b), C.byref(t), C.byref(m)))
+        return {"probe_first_ms": round(a.value, 4), "probe_final_ms": round(b.value, 4),
+                "tries": t.value, "moves": m.value}
+
     def reset(self) -> None:
         check(self.lib.cloudsc_state_reset(self.h))
 
@@ -661,6 +676,14 @@ class HostPipeline:
         n, bad = C.c_int(), C.c_int()
         check(self.lib.cloudsc_debug_host_pipeline_mapping(self.h, C.byref(n), C.byref(bad)))
         return n.value, bad.value
+
+    def copy_path(self):
+        """(mode, H2D engine mask, D2H engine mask) of this pipeline
+        (cloudsc_debug_host_pipeline_copy): mode 1 = copy engines per direction,
+        0 = HIP streams."""
+        m, a, b = C.c_int(), C.c_int(), C.c_int()
+        check(self.lib.cloudsc_debug_host_pipeline_copy(self.h, C.byref(m), C.byref(a), C.byref(b)))
+        return m.value, a.value, b.value
 
     def host_arrays(self):
         """(pointer, bytes) of every host array handed to the pipeline."""

@@ -1,13 +1,17 @@
 // cloudsc_pipeline.hip -- the host-buffer pipeline of include/cloudsc_amd.h
 // (cloudsc_host_pipeline_*).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include <unistd.h>
@@ -80,7 +84,7 @@ size_t per_block_elems(int kind, int nproma, int klev) {
 }  // namespace
 
 // D2H of one chunk by a copy kernel instead of the copy engine (diagnostic
-// mode, cloudsc_debug_set_pipeline_d2h_blit): every output field's chunk range,
+// mode 2 of cloudsc_debug_set_pipeline_copy): every output field's chunk range,
 // device buffer -> pinned host memory through its device-visible address, in
 // one launch.  16-byte accesses where both ends are 16-byte aligned, else 4 B.
 constexpr int kMaxBlitSeg = 24;
@@ -108,7 +112,91 @@ __global__ void __launch_bounds__(256) d2h_blit_kernel(const BlitSegs s) {
     }
   }
 }
-std::atomic<int> g_pipe_d2h_blit{0};
+// how the pipeline moves data (cloudsc_debug_set_pipeline_copy): 1 (default)
+// copy engines chosen explicitly through HSA, one per direction; 0 HIP streams
+// (the runtime picks the engines); 2 HIP streams with the outputs written back
+// by a copy kernel instead of a copy engine
+enum PipeCopy { PC_HIP = 0, PC_ENGINES = 1, PC_HIP_BLIT = 2 };
+std::atomic<int> g_pipe_copy{PC_ENGINES};
+
+// ---------------------------------------------------------------------------
+// Copy engines per direction (round 4).  Through hipMemcpyAsync the runtime
+// picks an SDMA engine per stream from the engines free at the moment it asks
+// (the recommended ones first: engine 0 for host->device, 1-2 for
+// device->host on MI355X).  When the host->device stream asks while engine 0 is
+// busy it lands on engine 1 -- the device->host stream's engine -- and the two
+// directions run one after the other: steps of 177-343 ms instead of 104 for
+// the same work, in runs of several steps (a copy trace shows zero overlap of
+// the two directions in the slow steps; profiles/r04/pipeline_engines.txt).  So
+// the pipeline issues its copies itself, with hsa_amd_memory_async_copy_on_engine,
+// H2D and D2H each on its own engine chosen once at creation, and orders them
+// with the kernels from the host: chunk c's inputs go in when the kernel of
+// chunk c - nslots has finished with the slot, chunk c-1's outputs go out as
+// soon as its kernel has finished, and chunk c's kernel starts once its inputs
+// are in and chunk c - nslots's outputs are out.  The copies of one direction
+// queue back to back on their engine, so the host's reaction time only adds
+// at the ends of the pipeline.
+struct HsaEngines {
+  bool ok = false;
+  hsa_agent_t cpu{}, gpu{};
+  hsa_amd_sdma_engine_id_t h2d{}, d2h{};
+};
+
+struct AgentSearch {
+  uint32_t bdfid, domain;
+  hsa_agent_t cpu{}, gpu{};
+  bool have_cpu = false, have_gpu = false;
+};
+
+hsa_status_t agent_cb(hsa_agent_t a, void* data) {
+  auto* q = (AgentSearch*)data;
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_CPU && !q->have_cpu) { q->cpu = a; q->have_cpu = true; }
+  if (t == HSA_DEVICE_TYPE_GPU) {
+    uint32_t bdf = 0, dom = 0;
+    if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS &&
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS &&
+        bdf == q->bdfid && dom == q->domain) {
+      q->gpu = a;
+      q->have_gpu = true;
+    }
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// the lowest engine of `mask` other than `not_this` (0 when none)
+uint32_t pick_engine(uint32_t mask, uint32_t not_this) {
+  for (uint32_t b = 1; b && b <= mask; b <<= 1)
+    if ((mask & b) && b != not_this) return b;
+  return 0;
+}
+
+HsaEngines find_engines(int device) {
+  HsaEngines e;
+  static std::once_flag once;
+  static bool hsa_up = false;
+  std::call_once(once, [] { hsa_up = hsa_init() == HSA_STATUS_SUCCESS; });   // HIP's runtime: a reference
+  if (!hsa_up) return e;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return e;
+  AgentSearch q;
+  q.bdfid = ((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3);
+  q.domain = (uint32_t)prop.pciDomainID;
+  if (hsa_iterate_agents(agent_cb, &q) != HSA_STATUS_SUCCESS || !q.have_cpu || !q.have_gpu) return e;
+  uint32_t rec_in = 0, rec_out = 0;
+  if (hsa_amd_memory_get_preferred_copy_engine(q.gpu, q.cpu, &rec_in) != HSA_STATUS_SUCCESS) rec_in = 0;
+  if (hsa_amd_memory_get_preferred_copy_engine(q.cpu, q.gpu, &rec_out) != HSA_STATUS_SUCCESS) rec_out = 0;
+  uint32_t in = pick_engine(rec_in ? rec_in : 0x1, 0);
+  uint32_t out = pick_engine(rec_out ? rec_out : 0x6, in);
+  if (!out) out = pick_engine(0xffff, in);
+  if (!in || !out) return e;
+  e.cpu = q.cpu; e.gpu = q.gpu;
+  e.h2d = (hsa_amd_sdma_engine_id_t)in;
+  e.d2h = (hsa_amd_sdma_engine_id_t)out;
+  e.ok = true;
+  return e;
+}
 
 struct cloudsc_host_pipeline {
   int device, precision, ngptot, nproma, klev, nblocks, chunk_blocks, nstreams;   // nstreams: device slots
@@ -124,7 +212,9 @@ struct cloudsc_host_pipeline {
   };
   std::vector<Slot> slots;
   hipStream_t st_in = nullptr, st_k = nullptr, st_out = nullptr;
-  void* host_dev[kNumFields] = {};   // device-visible addresses of the pinned host arrays (D2H by blit kernel)
+  void* host_dev[kNumFields] = {};   // agent (device-visible) addresses of the pinned host arrays
+  HsaEngines eng;                    // copy engines per direction (PC_ENGINES)
+  std::vector<hsa_signal_t> sig_in, sig_out;   // per slot: its chunk's copies still running
   std::vector<void*> allocs;
   ParamSet params;          // snapshot of the device's default set at creation
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -193,6 +283,99 @@ int pin_host_fields(cloudsc_host_pipeline* p, void* const* hf) {
   return CLOUDSC_OK;
 }
 
+// one step with every copy on the engines of p->eng (HsaEngines above); the
+// host orders copies and kernels
+int run_on_engines(cloudsc_host_pipeline* p, int variant, int vk, double* ms) {
+  const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
+  const int nslots = (int)p->slots.size();
+  const void* const* hf = (const void* const*)&p->host;
+  HIPCHK(hipDeviceSynchronize());
+  const auto t0 = std::chrono::steady_clock::now();
+  // the copies of chunk c in one direction, counted down on the slot's signal
+  auto issue = [&](int c, bool in) -> int {
+    auto& s = p->slots[c % nslots];
+    hsa_signal_t sg = in ? p->sig_in[c % nslots] : p->sig_out[c % nslots];
+    const int b0 = c * p->chunk_blocks;
+    const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
+    void* const* df = (void* const*)&s.dev;
+    int n = 0;
+    for (int i = 0; i < kNumFields; i++) {
+      const int dir = kFieldTable[i].dir;
+      if (hf[i] && (in ? dir != FD_OUT : (dir == FD_OUT || dir == FD_INOUT))) n++;
+    }
+    hsa_signal_store_screlease(sg, n);
+    for (int i = 0; i < kNumFields; i++) {
+      const FieldDesc& d = kFieldTable[i];
+      if (!hf[i] || !(in ? d.dir != FD_OUT : (d.dir == FD_OUT || d.dir == FD_INOUT))) continue;
+      const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * (d.is_int ? sizeof(int) : p->es);
+      char* h = (char*)p->host_dev[i] + (size_t)b0 * per;
+      const hsa_status_t st =
+          in ? hsa_amd_memory_async_copy_on_engine(df[i], p->eng.gpu, h, p->eng.cpu, (size_t)nb * per, 0, nullptr, sg,
+                                                   p->eng.h2d, true)
+             : hsa_amd_memory_async_copy_on_engine(h, p->eng.cpu, df[i], p->eng.gpu, (size_t)nb * per, 0, nullptr, sg,
+                                                   p->eng.d2h, true);
+      if (st != HSA_STATUS_SUCCESS) {
+        hsa_signal_subtract_screlease(sg, n);   // the copies not issued (the issued ones still count down)
+        set_error_text("host pipeline: hsa_amd_memory_async_copy_on_engine failed");
+        return CLOUDSC_EHIP;
+      }
+      n--;
+    }
+    return CLOUDSC_OK;
+  };
+  // 0 when every copy counted on sg is done; < 0 when one failed
+  auto wait = [](hsa_signal_t sg) {
+    return hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) == 0
+               ? CLOUDSC_OK : CLOUDSC_EHIP;
+  };
+  int rc = CLOUDSC_OK;
+  for (int c = 0; c < nchunks && rc == CLOUDSC_OK; c++) {
+    auto& s = p->slots[c % nslots];
+    const bool reuse = c >= nslots;        // the slot held chunk c - nslots
+    // inputs: after the slot's previous kernel has read its inputs
+    if (reuse && hipEventSynchronize(s.k_done) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
+    if ((rc = issue(c, true))) break;
+    // the previous chunk's outputs, as soon as its kernel is done
+    if (c >= 1) {
+      if (hipEventSynchronize(p->slots[(c - 1) % nslots].k_done) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
+      if ((rc = issue(c - 1, false))) break;
+    }
+    // kernel: after its inputs are in and the slot's previous outputs are out
+    if ((rc = wait(p->sig_in[c % nslots]))) break;
+    if (reuse && (rc = wait(p->sig_out[c % nslots]))) break;
+    const int b0 = c * p->chunk_blocks;
+    const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
+    const long long col0 = (long long)b0 * p->nproma;
+    const int ncols = (int)((col0 + (long long)nb * p->nproma <= p->ngptot) ? (long long)nb * p->nproma
+                                                                            : p->ngptot - col0);
+    if ((rc = gpu_run_impl(p->device, p->st_k, p->precision, variant, ncols, p->nproma, p->klev, &s.dev, s.scratch,
+                           nullptr, &p->params)))
+      break;
+    if (hipEventRecord(s.k_done, p->st_k) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
+  }
+  if (rc == CLOUDSC_OK) {
+    if (hipEventSynchronize(p->slots[(nchunks - 1) % nslots].k_done) != hipSuccess) rc = CLOUDSC_EHIP;
+    else rc = issue(nchunks - 1, false);
+  }
+  // every copy issued, finished (also after a failure: the slots are reused)
+  for (auto* v : {&p->sig_in, &p->sig_out})
+    for (hsa_signal_t sg : *v) {
+      const int r = wait(sg);
+      if (r && !rc) rc = r;
+    }
+  if (hipStreamSynchronize(p->st_k) != hipSuccess && !rc) rc = CLOUDSC_EHIP;
+  const auto t1 = std::chrono::steady_clock::now();
+  if (rc) return rc;
+  if (vk == CLOUDSC_VARIANT_KSEG)
+    for (auto& s : p->slots) {
+      const int r = kseg_check(p->device, p->st_k, s.scratch);
+      if (r && !rc) rc = r;
+    }
+  if (rc) return rc;
+  if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  return CLOUDSC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -247,6 +430,18 @@ int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int 
     }
   }
   if (hipEventCreate(&p->ev0) != hipSuccess || hipEventCreate(&p->ev1) != hipSuccess) return fail(CLOUDSC_EHIP);
+  // copy engines per direction: every array needs its agent address
+  bool all_dev = true;
+  for (int i = 0; i < kNumFields; i++) all_dev = all_dev && (!hf[i] || p->host_dev[i]);
+  if (all_dev) p->eng = find_engines(device);
+  if (p->eng.ok) {
+    for (auto* v : {&p->sig_in, &p->sig_out})
+      for (size_t k = 0; k < p->slots.size(); k++) {
+        hsa_signal_t sg;
+        if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) { p->eng.ok = false; break; }
+        v->push_back(sg);
+      }
+  }
   *out = p;
   return CLOUDSC_OK;
 }
@@ -274,6 +469,8 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
     }
     s.scratch_variant = vk;
   }
+  if (p->eng.ok && g_pipe_copy.load(std::memory_order_relaxed) == PC_ENGINES)
+    return run_on_engines(p, variant, vk, ms);
   const void* const* hf = (const void* const*)&p->host;
   // the three streams start after ev0 (recorded on the null stream) and ev1 waits for all of them
   HIPCHK(hipDeviceSynchronize());
@@ -309,7 +506,7 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
     // outputs (and plude): after the kernel
     HIPCHK(hipStreamWaitEvent(p->st_out, s.k_done, 0));
     BlitSegs bs{};
-    bool blit = g_pipe_d2h_blit.load(std::memory_order_relaxed) != 0;
+    const bool blit = g_pipe_copy.load(std::memory_order_relaxed) == PC_HIP_BLIT;
     for (int i = 0; i < kNumFields; i++) {
       const FieldDesc& d = kFieldTable[i];
       if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
@@ -364,6 +561,12 @@ int cloudsc_host_pipeline_destroy(cloudsc_host_pipeline_t* p) {
     for (hipEvent_t e : {s.in_done, s.k_done, s.out_done})
       if (e) (void)hipEventDestroy(e);
   for (void* q : p->allocs) (void)hipFree(q);
+  for (auto* v : {&p->sig_in, &p->sig_out})
+    for (hsa_signal_t sg : *v) {
+      // a failed step may leave copies running: let them finish before the memory goes
+      hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+      (void)hsa_signal_destroy(sg);
+    }
   for (void* h : p->pinned) (void)hipHostUnregister(h);
   param_set_free(&p->params);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
@@ -387,8 +590,18 @@ int cloudsc_debug_host_pipeline_mapping(const cloudsc_host_pipeline_t* p, int* n
   return CLOUDSC_OK;
 }
 
-int cloudsc_debug_set_pipeline_d2h_blit(int on) {
-  g_pipe_d2h_blit.store(on ? 1 : 0, std::memory_order_relaxed);
+int cloudsc_debug_set_pipeline_copy(int mode) {
+  if (mode < 0) mode = PC_ENGINES;
+  if (mode > PC_HIP_BLIT) return CLOUDSC_EINVAL;
+  g_pipe_copy.store(mode, std::memory_order_relaxed);
+  return CLOUDSC_OK;
+}
+
+int cloudsc_debug_host_pipeline_copy(const cloudsc_host_pipeline_t* p, int* mode, int* h2d_engine, int* d2h_engine) {
+  if (!p) return CLOUDSC_EINVAL;
+  if (mode) *mode = p->eng.ok ? PC_ENGINES : PC_HIP;
+  if (h2d_engine) *h2d_engine = p->eng.ok ? (int)p->eng.h2d : 0;
+  if (d2h_engine) *d2h_engine = p->eng.ok ? (int)p->eng.d2h : 0;
   return CLOUDSC_OK;
 }
 

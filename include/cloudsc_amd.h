@@ -342,6 +342,24 @@ int cloudsc_state_create(cloudsc_gpu_state_t **state, int device, int precision,
  * default parameter set, not the state's). */
 int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out);
 
+/* How the state's output fields were placed (round 4).  The rate at which
+ * the kernel writes its 21 output fields depends on where they land in HBM
+ * (fp64 KSEG 1.63-1.94 ms for states of one configuration: fields written
+ * together whose physical pages collide stall on DRAM write credits).  At
+ * creation the state times the KSEG kernel on its own inputs over candidate
+ * placements of its outputs -- whole fresh output sets, then one field at a
+ * time -- and keeps a candidate when the time drops by more than 1 %.
+ * probe_first_ms / probe_final_ms: the kernel time of the first / the kept
+ * placement, tries / moves: output buffers allocated as candidates / kept.
+ * All zero when the search was off.  Any pointer may be NULL. */
+int cloudsc_state_placement(const cloudsc_gpu_state_t *state, float *probe_first_ms, float *probe_final_ms,
+                            int *tries, int *moves);
+
+/* Diagnostic: passes of the output placement search of the states created
+ * after this call (0 = off: the first allocation is kept; negative = the
+ * default, 2; at most 8).  The results do not depend on it. */
+int cloudsc_debug_set_placement_search(int passes);
+
 /* Diagnostic: move field `member` (its position in cloudsc_fields_t) of a state
  * to a new device allocation, contents copied; the old allocation is kept until
  * the state is destroyed, so the field lands on other physical pages.  For
@@ -432,11 +450,24 @@ int cloudsc_debug_host_pipeline_mapping(const cloudsc_host_pipeline_t *pipe, int
  * it was destroyed). */
 int cloudsc_debug_host_pinned(const void *ptr, long long bytes);
 
-/* Diagnostic: host pipelines run after this call copy their outputs back with
- * a copy kernel writing the pinned host memory through its device-visible
- * address (on = 1) instead of the copy engine (0, the default); for measuring
- * the two directions' overlap (tools/pipeline_steps.py). */
-int cloudsc_debug_set_pipeline_d2h_blit(int on);
+/* Diagnostic: how host pipeline steps run after this call move their data.
+ * 1 (the default; negative restores it): every copy issued by the pipeline on
+ * a copy engine of its own per direction (hsa_amd_memory_async_copy_on_engine,
+ * engines chosen at creation), ordered with the kernels from the host -- the
+ * runtime's own engine choice for hipMemcpyAsync lets both directions land on
+ * one engine now and then, which serialises them (~1.7-3.3x slower steps,
+ * profiles/r04/pipeline_engines.txt).  0: three HIP streams (one per
+ * direction, one for the kernels) with the runtime's engine choice.  2: as 0,
+ * with the outputs written back by a copy kernel through the pinned memory's
+ * device address.  A pipeline whose engines could not be set up at creation
+ * runs as 0.  CLOUDSC_EINVAL for other modes. */
+int cloudsc_debug_set_pipeline_copy(int mode);
+
+/* Diagnostic: the copy path a pipeline was set up with: *mode 1 with the
+ * engine masks (hsa_amd_sdma_engine_id_t bits) it copies on per direction, or
+ * 0 (HIP streams) with both masks 0.  Any output pointer may be NULL. */
+int cloudsc_debug_host_pipeline_copy(const cloudsc_host_pipeline_t *pipe, int *mode, int *h2d_engine,
+                                     int *d2h_engine);
 
 /* ------------------------------------------------------------------------ */
 /* One synchronous step on host arrays, callable from any host thread        */

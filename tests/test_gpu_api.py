@@ -312,6 +312,36 @@ def test_state_field_placement_is_transparent(lib, ds):
 
 
 @pytest.mark.parametrize("precision", [ca.FP64, ca.FP32])
+def test_output_placement_search(lib, ds, precision):
+    """The output placement search at state creation (cloudsc_state_placement)
+    moves output buffers before anything is written to them: a state created
+    with it (the default, and with 4 passes) computes exactly what a state
+    created without it computes, KSEG and KCACHE; its record is consistent
+    (the kept time no worse than the first, moves <= tries), and with the
+    search off the record is all zero."""
+    assert lib.cloudsc_debug_set_placement_search(9) == ca.EINVAL
+    out, rec = [], []
+    try:
+        for passes in (0, -1, 4):
+            ca.check(lib.cloudsc_debug_set_placement_search(passes))
+            g = ca.GpuState(ds, 3000, 64, precision)
+            try:
+                rec.append(g.placement())
+                out.append(outputs_of(g, ca.VARIANT_KSEG))
+                out.append(outputs_of(g, ca.VARIANT_KCACHE))
+            finally:
+                g.close()
+    finally:
+        ca.check(lib.cloudsc_debug_set_placement_search(-1))
+    for j in range(1, len(out)):
+        assert bitwise_mismatches(out[0], out[j]) == {}, j
+    assert rec[0] == {"probe_first_ms": 0.0, "probe_final_ms": 0.0, "tries": 0, "moves": 0}
+    for r in rec[1:]:
+        assert 0 < r["probe_final_ms"] <= r["probe_first_ms"]
+        assert 0 <= r["moves"] <= r["tries"] and r["tries"] >= 21
+
+
+@pytest.mark.parametrize("precision", [ca.FP64, ca.FP32])
 def test_kseg_shared_workspace_alternating_states(lib, ds, precision):
     """Two states with different inputs (B = the template's columns rotated by
     half, so every block carries other values between its segments) run

@@ -390,6 +390,34 @@ def test_host_pipeline_fp32(lib, ds):
         assert np.array_equal(out[k], ref[k]), k
 
 
+@pytest.mark.parametrize("variant", [ca.VARIANT_KSEG, ca.VARIANT_KCACHE])
+def test_host_pipeline_copy_paths(lib, ds, variant):
+    """Every copy path of the pipeline (cloudsc_debug_set_pipeline_copy: copy
+    engines pinned per direction -- the default --, HIP streams, HIP streams
+    with a copy kernel for the outputs) gives the resident bits, over chunks
+    whose slots are reused (7 chunks on 3 slots, the last one partial).  The
+    default path runs on two different engines."""
+    ref = run_gpu(ds, 1000, 64, variant=ca.VARIANT_KCACHE)
+    assert lib.cloudsc_debug_set_pipeline_copy(3) == ca.EINVAL
+    try:
+        for mode in (1, 0, 2):
+            ca.check(lib.cloudsc_debug_set_pipeline_copy(mode))
+            hp = ca.HostPipeline(ds, 1000, 64, chunk_blocks=2, nstreams=3)
+            try:
+                m, e_in, e_out = hp.copy_path()
+                if mode == 1:
+                    assert m == 1 and e_in and e_out and e_in != e_out, (m, e_in, e_out)
+                hp.run(variant)
+                hp.run(variant)
+                out = hp.outputs()
+            finally:
+                hp.close()
+            for _, k in ca.VALIDATED:
+                assert np.array_equal(out[k], ref[k]), (mode, k)
+    finally:
+        ca.check(lib.cloudsc_debug_set_pipeline_copy(-1))
+
+
 # ---- shapes beyond the reference's: other KLEV, tiny and ragged problems ----
 def sliced_levels(ds, lo_lev):
     import make_fixtures as mf

@@ -3,10 +3,11 @@
 (cloudsc_host_pipeline_run) -- every step's time, for host arrays from numpy
 (pinned in place by the pipeline with hipHostRegister) and for the same arrays
 in hipHostMalloc memory (already pinned; the pipeline uses them as they are),
-with the outputs copied back by the copy engine or by a copy kernel
-(cloudsc_debug_set_pipeline_d2h_blit).
+and by copy path (cloudsc_debug_set_pipeline_copy): engines pinned per
+direction (the default), HIP streams with the runtime's engine choice, or HIP
+streams with the outputs written back by a copy kernel.
 usage: pipeline_steps.py [steps] [chunk_blocks] [slots] [modes]
-modes: comma-separated of reg, reg-blit, hm, hm-blit (default: all, then reg again)"""
+modes: comma-separated of reg, reg-hip, reg-blit, hm, hm-hip (default: reg, reg-hip, hm, hm-hip, reg)"""
 import ctypes as C
 import json
 import os
@@ -27,8 +28,11 @@ hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
 hip.hipHostFree.argtypes = [C.c_void_p]
 
 
-def run(kind, blit=0):
-    ca.gpu_lib().cloudsc_debug_set_pipeline_d2h_blit(blit)
+COPY = {0: "hip streams", 1: "engines per direction", 2: "hip streams, D2H by copy kernel"}
+
+
+def run(kind, copy=1):
+    ca.check(ca.gpu_lib().cloudsc_debug_set_pipeline_copy(copy))
     hp = ca.HostPipeline.__new__(ca.HostPipeline)
     if kind == "registered":
         hp = ca.HostPipeline(ds, 163840, 64, ca.FP64, chunk_blocks=chunk, nstreams=slots)
@@ -64,14 +68,14 @@ def run(kind, blit=0):
         hp.close()
         for p in keep:
             hip.hipHostFree(p)
-    print(json.dumps({"host_memory": kind, "d2h": "blit kernel" if blit else "copy engine",
+    print(json.dumps({"host_memory": kind, "copy": COPY[copy],
                       "chunk_blocks": chunk, "slots": slots, "ms": ms,
                       "median": float(np.median(ms)), "min": min(ms)}), flush=True)
 
 
-MODES = {"reg": ("registered", 0), "reg-blit": ("registered", 1), "hm": ("hostmalloc", 0),
-         "hm-blit": ("hostmalloc", 1)}
-modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["reg", "reg-blit", "hm", "hm-blit", "reg"]
+MODES = {"reg": ("registered", 1), "reg-hip": ("registered", 0), "reg-blit": ("registered", 2),
+         "hm": ("hostmalloc", 1), "hm-hip": ("hostmalloc", 0)}
+modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["reg", "reg-hip", "hm", "hm-hip", "reg"]
 for m in modes:
     run(*MODES[m])
-ca.gpu_lib().cloudsc_debug_set_pipeline_d2h_blit(0)
+ca.check(ca.gpu_lib().cloudsc_debug_set_pipeline_copy(-1))

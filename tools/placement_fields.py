@@ -47,12 +47,15 @@ def main():
     p.add_argument("--rounds", type=int, default=20)
     p.add_argument("--warmup", type=int, default=15)
     p.add_argument("--reroll", type=int, default=3)
+    p.add_argument("--search", type=int, default=0, help="placement search passes at creation (0: off)")
     a = p.parse_args()
     prec = ca.FP64 if a.precision == "fp64" else ca.FP32
     lib = ca.gpu_lib()
     lib.cloudsc_debug_state_relocate_field.argtypes = [C.c_void_p, C.c_int]
     ds = ca.load_dataset()
+    ca.check(lib.cloudsc_debug_set_placement_search(a.search))
     states = [ca.GpuState(ds, a.ngptot, a.nproma, prec) for _ in range(a.reps)]
+    ca.check(lib.cloudsc_debug_set_placement_search(-1))
     names = [n for n, _ in ca.Fields._fields_]
     try:
         interleaved(states, a.warmup)
