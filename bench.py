@@ -150,7 +150,7 @@ def roofline_traffic(ca, path, key):
 
 def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
     """Host-resident block-layout arrays (pinned in place), per chunk H2D ->
-    kernel -> D2H pipelined over an input, a kernel and an output stream: the
+    kernel -> D2H pipelined over the two directions' copy engines and a kernel stream: the
     reference GPU drivers' TOTAL semantics (cloudsc_driver.cu:344-456).  plude
     is restored on the host between steps, outside the timed pipeline.  The
     default chunking is the measured best (profiles/r04/transfer_sweep_kseg_fp64.txt).
@@ -160,6 +160,7 @@ def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
     pc = ca.pcie_gbps(0, 1 << 30, 3)
     hp = ca.HostPipeline(ds, args.ngptot, args.nproma, prec, chunk_blocks=chunk_blocks, nstreams=slots)
     try:
+        mode, e_in, e_out = hp.copy_path()
         hp.run(variant)
         ms = [hp.run(variant) for _ in range(args.transfer_steps)]
     finally:
@@ -174,7 +175,10 @@ def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
     return {"value": round(args.ngptot / (t * 1e-3), 1), "unit": "columns/s", "ms_per_step": round(t, 3),
             "ms_per_step_method": "median of the timed steps", "ms_per_step_mean": round(sum(ms) / len(ms), 3),
             "ms_per_step_min": round(min(ms), 3), "ms_per_step_all": [round(x, 2) for x in ms], "steps": len(ms),
-            "chunk_blocks": chunk_blocks, "slots": slots, "streams": "one H2D, one kernel, one D2H",
+            "chunk_blocks": chunk_blocks, "slots": slots,
+            "copies": ("every copy on a copy engine of its own per direction (H2D engine mask 0x%x, D2H 0x%x), "
+                       "ordered with the kernels from the host" % (e_in, e_out)) if mode == 1 else
+                      "one H2D, one kernel, one D2H HIP stream (the runtime picks the copy engines)",
             "bytes_per_step": BYTES_PER_COL[prec] * args.ngptot, "bytes_in": in_b, "bytes_out": out_b,
             "copy_ceiling_gbs": {k: round(v, 1) for k, v in pc.items()},
             "bound_ms": round(bound_ms, 2), "frac_of_bound": round(bound_ms / t, 4),

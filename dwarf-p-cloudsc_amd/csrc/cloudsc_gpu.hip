@@ -241,7 +241,12 @@ namespace {
 // (tools/sweep.py); the product library never reads the environment.
 template <typename real> struct DefaultCfg;
 template <> struct DefaultCfg<double> { static constexpr int code = 23, waves = 2, pf = 3; };
-template <> struct DefaultCfg<float> { static constexpr int code = 21, waves = 2, pf = 1; };
+#ifndef CLOUDSC_FP32_PF   // experiment builds: the fp32 load schedule (make variant VFLAGS=-DCLOUDSC_FP32_PF=3)
+#define CLOUDSC_FP32_PF 1
+#endif
+template <> struct DefaultCfg<float> {
+  static constexpr int code = 20 + CLOUDSC_FP32_PF, waves = 2, pf = CLOUDSC_FP32_PF;
+};
 
 #ifdef CLOUDSC_DEBUG_KNOBS
 // code: [1]<waves><pf> -- leading 1 = carried state in LDS
