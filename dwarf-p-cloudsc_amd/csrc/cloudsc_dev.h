@@ -495,13 +495,23 @@ CLOUDSC_HD real cl_div(typename std::common_type<real>::type n, typename std::co
 // reciprocal and two corrections, which make every quotient the IEEE one).
 // The correction leaves q within 1 ulp of n/d (almost always the IEEE
 // quotient).  fp64 and the exact fp32 forms (CLOUDSC_FP32_EXACT_LIBM) are cl_div.
+// Valid range of the fast forms (no div_scale / div_fixup): a divisor with
+// 2^-126 <= |d| < 2^126 (a normal float whose reciprocal is normal) and a
+// quotient that is finite and normal; then 0/d = 0 exactly and every other
+// quotient is within 1 ulp.  A smaller |d| makes v_rcp_f32 overflow, so the
+// result is NaN (0/d) or inf/NaN where IEEE gives a finite value; zero and
+// non-finite divisors give NaN.  Every division of the physics has a divisor in
+// that range: max(x, epsilon) clamps, 1 + positive sums, temperatures and
+// pressures (tests/test_gpu_parity.py::test_fp32_fast_division_range checks
+// the contract and the out-of-range behaviour on the device).
+__device__ __forceinline__ float cl_divf_fast(float n, float d) {
+  const float r = __builtin_amdgcn_rcpf(d), q = n * r;
+  return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+}
 template <typename real, typename P>
 CLOUDSC_HD real cl_div_p(const P&, typename std::common_type<real>::type n, typename std::common_type<real>::type d) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (LibmFast<P>::value) {
-    const float r = __builtin_amdgcn_rcpf(d), q = n * r;
-    return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
-  }
+  if constexpr (LibmFast<P>::value) return cl_divf_fast(n, d);
 #endif
   return cl_div(static_cast<real>(n), static_cast<real>(d));
 }

@@ -750,13 +750,15 @@ __global__ void __launch_bounds__(256) fp32_libm_kernel(int which, const float* 
     case 0: r = cl_expf_fast(x[i]); break;
     case 1: r = cl_powf_fast(x[i], y[i]); break;
     case 2: r = cl_exp_impl(x[i]); break;
-    default: r = cl_powr(x[i], y[i]); break;
+    case 3: r = cl_powr(x[i], y[i]); break;
+    case 4: r = cl_divf_fast(x[i], y[i]); break;     // the fast kernels' x / y
+    default: r = cl_div(x[i], y[i]); break;          // the exact kernels' x / y
   }
   out[i] = r;
 }
 
 int cloudsc_debug_fp32_libm(int device, int which, const float* x, const float* y, float* out, long long n) {
-  if (which < 0 || which > 3 || !x || !out || n <= 0 || ((which & 1) && !y)) return CLOUDSC_EINVAL;
+  if (which < 0 || which > 5 || !x || !out || n <= 0 || ((which & 1 || which >= 4) && !y)) return CLOUDSC_EINVAL;
   int nd = 0;
   if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return CLOUDSC_ENODEV;
   HIPCHK(hipSetDevice(device));

@@ -351,6 +351,15 @@ constexpr unsigned kAblate = CLOUDSC_ABLATE;
 #define CLOUDSC_RUN(bit) ((kAblate & (bit)) == 0)
 
 // ===== 3.-6. physics of one level ncldtop <= k (cloudsc_c.c:732-2508) =====
+// Where in the level physics_level calls its mid hook: 0 (the default) after
+// 5.1; experiment builds (VFLAGS=-DCLOUDSC_MID_AT=n) move it earlier -- 1 before
+// the Newton steps of 3.4, 2 before 3.7, 3 before 4.2, 4 before 4.4, 5 before
+// 4.5 -- trading a longer flight time of the next level's loads against their
+// registers being live across more of the physics.
+#ifndef CLOUDSC_MID_AT
+#define CLOUDSC_MID_AT 0
+#endif
+#define CLOUDSC_MID_HOOK(n) do { if constexpr (CLOUDSC_MID_AT == (n)) mid(); } while (0)
 // Nothing to do at the middle of a level (the default hook of physics_level).
 struct NoMidHook {
   CLOUDSC_HD void operator()() const {}
@@ -551,6 +560,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       sa_iv = sa_iv + zicefrac * zleros;
     }
 
+    CLOUDSC_MID_HOOK(1);
     // 3.4 condensation/evaporation due to dqsat/dt: two Newton steps (:1137-1182)
     real zdqs;
     if (!CLOUDSC_RUN(AB_NEWTON)) {
@@ -648,6 +658,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
     }
 
+    CLOUDSC_MID_HOOK(2);
     // 3.7 growth of ice by vapour deposition, Rotstayn (:1382-1447)
     if (za >= c.rcldtopcf && cs.a_prev < c.rcldtopcf) cs.zcldtopdist = R(0.0);
     else cs.zcldtopdist = cs.zcldtopdist + cl_div_p<real>(c, zdp, (zrho * c.rg));
@@ -674,6 +685,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     zicecld = zqxfg[QI] * ztmpa;
     zlicld = zliqcld + zicecld;
 
+    CLOUDSC_MID_HOOK(3);
     // 4.2 sedimentation of ice, rain, snow (:1541-1576)
     if (CLOUDSC_RUN(AB_SEDIM) && k > ncldtop0) {
       fsrc_i = cs.pfx_i * zdtgdp; sa_ii = sa_ii + fsrc_i; zqxfg[QI] = zqxfg[QI] + fsrc_i; zqpretot = zqpretot + zqxfg[QI];
@@ -736,6 +748,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       sb_ls = sb_ls + zsnowrime;
     }
 
+    CLOUDSC_MID_HOOK(4);
     // 4.4a melting of snow and ice (:1817-1859)
     const real zicetot = zqxfg[QI] + zqxfg[QS];
     if (CLOUDSC_RUN(AB_MELT) && zicetot > zepsec && ztp1 > c.rtt) {
@@ -790,6 +803,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
       }
     }
 
+    CLOUDSC_MID_HOOK(5);
     // 4.5 evaporation of rain, Abel and Boutle (:1982-2040).  The humidity
     // threshold zzrh0, zqsliq and zqe are pure functions of values fixed by now
     // (cs.zcovpmax is not changed by either evaporation): they are evaluated
@@ -852,7 +866,7 @@ CLOUDSC_HD void physics_level(const P& c, const int k, const int klev,
     cs.zanewm1 = zanew;
     // the hook: the k-caching kernel issues the next level's first-consumed
     // loads here (PF 3), after the physics' peak of live temporaries
-    mid();
+    CLOUDSC_MID_HOOK(0);
 
     // 5.2 truncate explicit sinks, species in order (:2233-2286).
     // Column m of zsolqa (zsolqa[n][m], n=0..4) in C indexing; for each m the

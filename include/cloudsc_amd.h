@@ -221,7 +221,8 @@ int cloudsc_debug_set_state_layout(long long stagger, unsigned alloc_flags);
 /* Diagnostic: the kernels' single-precision exp/pow on the device, element-wise
  * over n host values: which = 0 the float-internal expf (CLOUDSC_FP32 default),
  * 1 its powf(x, y), 2 the glibc-algorithm expf (CLOUDSC_FP32_EXACT_LIBM),
- * 3 its powf.  y is read for 1 and 3 only. */
+ * 3 its powf, 4 the fast kernels' division x / y (v_rcp_f32 + one correction),
+ * 5 the exact kernels' division.  y is read for 1, 3, 4 and 5 only. */
 int cloudsc_debug_fp32_libm(int device, int which, const float *x, const float *y, float *out, long long n);
 
 /* Human-readable message for an error code; last HIP error string of this thread. */

@@ -687,6 +687,12 @@ def test_bitwise_fp32_other_configurations(lib, ds, oracle_mod, case, variant):
 # reference state and 6e-4..5e-3 on the perturbed / W / M states.  There the
 # gate is evidence-based: no field may move more than 2x the worst field of
 # that +-1-ulp probe (4 seeds), nor more than 1e-4 where the probe moves less.
+# The probe is calibrated on expf/powf only: the fast kernels also round every
+# division (1 ulp, cl_divf_fast), known-divisor division (1.5 ulp) and sqrt
+# (1 ulp) differently from the restatement, and those are not nudged.  That is
+# the same size of perturbation at more sites, so the floor can under-state the
+# fast kernels' legitimate spread; the fixed 1e-4 gate on the reference state
+# and test_fp32_fast_division_range below bound the divisions directly.
 RELL1_FP32_FAST = 1e-4
 
 
@@ -812,3 +818,41 @@ def test_fp32_fast_libm_special_values(lib):
         assert np.array_equal(np.isnan(fast), np.isnan(want)), (fast, want)
         assert np.array_equal(fast[~fin & ~np.isnan(want)], want[~fin & ~np.isnan(want)]), (fast, want)
         assert ulp_distance(fast[fin], ref[fin]).max() <= 2, (fast[fin], ref[fin])
+
+
+def test_fp32_fast_division_range(lib):
+    """The fast kernels' division (cl_divf_fast: v_rcp_f32 + one residual
+    correction, no div_scale / div_fixup) against IEEE float division, over its
+    documented range (cloudsc_dev.h): normal divisors 2^-126 <= |d| < 2^126
+    with finite normal quotients are within 1 ulp and 0/d is 0; the exact
+    kernels' division (cl_div) is the IEEE quotient everywhere in that range.
+    Outside it (|d| below 2^-126 where the reciprocal overflows, zero divisors)
+    the fast form is not IEEE; the test records that behaviour so a change shows."""
+    rng = np.random.default_rng(5)
+    n = 1 << 20
+    d = (np.sign(rng.uniform(-1, 1, n)) * 2.0 ** rng.uniform(-125.9, 125.9, n)).astype(np.float32)
+    num = (np.sign(rng.uniform(-1, 1, n)) * 2.0 ** rng.uniform(-60.0, 60.0, n)).astype(np.float32)
+    num[:1000] = 0.0
+    # CLOUDSC-like operands: ratios of physical quantities near 1e-12 .. 1e5
+    d[1000:200000] = (10.0 ** rng.uniform(-12.0, 5.0, 199000)).astype(np.float32)
+    with np.errstate(over="ignore", under="ignore"):
+        want = (num / d).astype(np.float32)
+    ok = np.isfinite(want) & ((want == 0) | (np.abs(want) >= np.finfo(np.float32).tiny))
+    out = {}
+    for which in (4, 5):
+        o = np.empty(n, np.float32)
+        ca.check(lib.cloudsc_debug_fp32_libm(0, which, num.ctypes.data, d.ctypes.data, o.ctypes.data, n))
+        out[which] = o
+    assert np.all(out[4][:1000] == 0.0)
+    dist = ulp_distance(out[4][ok], want[ok])
+    print("fast fp32 division: max %d ulp, %.2f %% IEEE" % (dist.max(), 100.0 * np.mean(dist == 0)))
+    assert dist.max() <= 1
+    mid = ok & (np.abs(want) >= 2.0 ** -100) & (np.abs(want) <= 2.0 ** 100)   # no residual underflow
+    assert np.array_equal(out[5][mid].view(np.int32), want[mid].view(np.int32))
+    # out of range: tiny / zero divisors (documented: not the IEEE answer)
+    tn = np.array([0.0, 1.0, 1e-30, 0.0, 1.0], np.float32)
+    td = np.array([1e-40, 1e-40, 1e-39, 0.0, 0.0], np.float32)
+    o = np.empty(tn.size, np.float32)
+    ca.check(lib.cloudsc_debug_fp32_libm(0, 4, tn.ctypes.data, td.ctypes.data, o.ctypes.data, tn.size))
+    print("fast fp32 division out of range:", list(zip(tn, td, o)))
+    assert not np.isfinite(o[0]) and not np.isfinite(o[3]), o
