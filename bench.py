@@ -294,8 +294,10 @@ def main():
         "sclk_method": "effective shader clock of the timed launches: each workgroup's s_memtime cycles over its "
                        "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",
         "placement": dict(per_rank[0]["placement"], method=(
-            "output placement search at state creation (cloudsc_state_placement): a write-only kernel with the "
-            "physics kernel's output pattern timed before / after moving output fields to fresh allocations; rank 0")),
+            "output placement search at state creation (cloudsc_state_placement): the KSEG kernel on the state's "
+            "own inputs timed (best of 2) over candidate output placements -- whole fresh output sets, then one "
+            "field at a time -- a candidate kept when it is > 1 % faster; probe ms of the first and the kept "
+            "placement; rank 0")),
         "per_rank": per_rank,
         "validation_worst_rel_l1": worst,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

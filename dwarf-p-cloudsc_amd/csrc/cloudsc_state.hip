@@ -287,8 +287,29 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
     }
     if (!moved) break;
   }
-  // the chosen buffers become the state's, the rest go back
   void** sf = (void**)&s->f;
+  // probes whose segment hand-offs timed out (the diagnostic spin limit, or a
+  // real fault of the schedule) timed nothing meaningful: keep the first
+  // placement, clear the workspace's error and record the search as abandoned
+  // (probe_final_ms < 0); a KSEG run of the state reports such a fault itself
+  if (rc == CLOUDSC_OK) {
+    const int hc = kseg_check(s->device, s->stream, s->kseg_ws);
+    if (hc == CLOUDSC_EHANDOFF) {
+      for (int q = 0; q < n; q++) {
+        const int m = members[q];
+        if (bf[m] == sf[m]) continue;
+        for (auto& h : held)
+          if (h == sf[m]) { h = held.back(); held.pop_back(); break; }
+        held.push_back(bf[m]);
+        bf[m] = sf[m];
+      }
+      s->place_moves = 0;
+      best = -1.f;
+    } else {
+      rc = hc;
+    }
+  }
+  // the chosen buffers become the state's, the rest go back
   for (int q = 0; q < n; q++) {
     if (bf[members[q]] == sf[members[q]]) continue;
     s->allocs.push_back(bf[members[q]]);
@@ -300,7 +321,6 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
     if (owned) dfree(s, p); else (void)hipFree(p);
   }
   s->place_final_ms = best;
-  if (rc == CLOUDSC_OK) rc = kseg_check(s->device, s->stream, s->kseg_ws);
   return rc;
 }
 

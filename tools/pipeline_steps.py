@@ -28,6 +28,38 @@ hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
 hip.hipHostFree.argtypes = [C.c_void_p]
 
 
+def host_nodes(arrays, per_array=8):
+    """NUMA node of sampled pages of the host arrays (move_pages(2) query
+    form, nothing is moved): {node: pages}."""
+    libc = C.CDLL(None, use_errno=True)
+    pages = []
+    for a in arrays.values():
+        if a.nbytes >= 4096:
+            base = a.ctypes.data
+            pages += [base + i * (a.nbytes // per_array) // 4096 * 4096 for i in range(per_array)]
+    n = len(pages)
+    pa = (C.c_void_p * n)(*pages)
+    st = (C.c_int * n)()
+    if libc.syscall(279, 0, C.c_ulong(n), pa, None, st, 0) != 0:   # SYS_move_pages (x86_64)
+        return None
+    out = {}
+    for v in st:
+        out[str(v)] = out.get(str(v), 0) + 1
+    return out
+
+
+def gpu_numa_node():
+    bus = C.create_string_buffer(64)
+    if hip.hipDeviceGetPCIBusId(bus, 64, 0) != 0:
+        return None
+    try:
+        return int(open("/sys/bus/pci/devices/%s/numa_node" % bus.value.decode().lower()).read())
+    except (OSError, ValueError):
+        return None
+
+
+GPU_NODE = gpu_numa_node()
+
 COPY = {0: "hip streams", 1: "engines per direction", 2: "hip streams, D2H by copy kernel"}
 
 
@@ -62,13 +94,16 @@ def run(kind, copy=1):
                                                   C.byref(f)))
         hp.h = h
     try:
+        mode, e_in, e_out = hp.copy_path()
+        nodes = host_nodes(hp.state.arrays)
         hp.run(ca.VARIANT_KSEG)
         ms = [round(hp.run(ca.VARIANT_KSEG), 2) for _ in range(steps)]
     finally:
         hp.close()
         for p in keep:
             hip.hipHostFree(p)
-    print(json.dumps({"host_memory": kind, "copy": COPY[copy],
+    print(json.dumps({"host_memory": kind, "copy": COPY[copy], "engines": [e_in, e_out],
+                      "host_numa_nodes": nodes, "gpu_numa_node": GPU_NODE,
                       "chunk_blocks": chunk, "slots": slots, "ms": ms,
                       "median": float(np.median(ms)), "min": min(ms)}), flush=True)
 
