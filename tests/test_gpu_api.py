@@ -101,8 +101,12 @@ def forced_handoff_failure():
 
 
 def test_handoff_timeout_state_api(lib, ds, forced_handoff_failure):
+    # the output placement search's own KSEG launches time out too: the state is
+    # still created, with its first placement (probe_final_ms < 0, no moves)
     g = ca.GpuState(ds, 2000, 64)
     try:
+        rec = g.placement()
+        assert rec["probe_final_ms"] < 0 and rec["moves"] == 0, rec
         rc = lib.cloudsc_state_run(g.h, ca.VARIANT_KSEG, 1, None)
         assert rc == ca.EHANDOFF, rc
         assert b"hand-off" in lib.cloudsc_last_hip_error()
