@@ -295,8 +295,9 @@ def main():
                        "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",
         "placement": dict(per_rank[0]["placement"], method=(
             "output placement search at state creation (cloudsc_state_placement): the KSEG kernel on the state's "
-            "own inputs timed (best of 2) over candidate output placements -- whole fresh output sets, then one "
-            "field at a time -- a candidate kept when it is > 1 % faster; probe ms of the first and the kept "
+            "own inputs timed (best of 2) over candidate placements -- whole fresh output sets, one output field at "
+            "a time, then whole fresh input sets -- a candidate kept when it is > 1 % faster; probe ms of the "
+            "first and the kept "
             "placement; rank 0")),
         "per_rank": per_rank,
         "validation_worst_rel_l1": worst,

@@ -349,7 +349,8 @@ int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out
  * together whose physical pages collide stall on DRAM write credits).  At
  * creation the state times the KSEG kernel on its own inputs over candidate
  * placements of its outputs -- whole fresh output sets, then one field at a
- * time -- and keeps a candidate when the time drops by more than 1 %.
+ * time -- then of its inputs (two whole fresh input sets, contents copied),
+ * and keeps a candidate when the time drops by more than 1 %.
  * If the search's launches time out in a segment hand-off, the first
  * placement is kept and probe_final_ms is negative (the state is created).
  * probe_first_ms / probe_final_ms: the kernel time of the first / the kept
