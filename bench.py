@@ -161,6 +161,7 @@ def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
     hp = ca.HostPipeline(ds, args.ngptot, args.nproma, prec, chunk_blocks=chunk_blocks, nstreams=slots)
     try:
         mode, e_in, e_out = hp.copy_path()
+        overlap, pairs = hp.engine_check()
         hp.run(variant)
         ms = [hp.run(variant) for _ in range(args.transfer_steps)]
     finally:
@@ -179,6 +180,9 @@ def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
             "copies": ("every copy on a copy engine of its own per direction (H2D engine mask 0x%x, D2H 0x%x), "
                        "ordered with the kernels from the host" % (e_in, e_out)) if mode == 1 else
                       "one H2D, one kernel, one D2H HIP stream (the runtime picks the copy engines)",
+            "engine_check": {"overlap": round(overlap, 3), "pairs_tried": pairs,
+                             "method": "at creation, 256 MiB each way at once / the slower direction alone on "
+                                       "the engine pair (1.0 = fully concurrent); first pair under 1.3 kept"},
             "bytes_per_step": BYTES_PER_COL[prec] * args.ngptot, "bytes_in": in_b, "bytes_out": out_b,
             "copy_ceiling_gbs": {k: round(v, 1) for k, v in pc.items()},
             "bound_ms": round(bound_ms, 2), "frac_of_bound": round(bound_ms / t, 4),

@@ -402,6 +402,8 @@ def gpu_lib(path: Optional[str] = None):
         lib.cloudsc_debug_set_pipeline_copy.argtypes = [C.c_int]
         lib.cloudsc_debug_host_pipeline_copy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                                          C.POINTER(C.c_int)]
+        lib.cloudsc_debug_host_pipeline_engine_check.argtypes = [C.c_void_p, C.POINTER(C.c_double),
+                                                                 C.POINTER(C.c_int)]
     lib.cloudsc_gpu_init.argtypes = [C.c_int, C.POINTER(Params)]
     lib.cloudsc_gpu_run.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.POINTER(Fields), C.c_void_p]
@@ -684,6 +686,14 @@ class HostPipeline:
         m, a, b = C.c_int(), C.c_int(), C.c_int()
         check(self.lib.cloudsc_debug_host_pipeline_copy(self.h, C.byref(m), C.byref(a), C.byref(b)))
         return m.value, a.value, b.value
+
+    def engine_check(self):
+        """(overlap, pairs tried) of the engine pair check at creation
+        (cloudsc_debug_host_pipeline_engine_check): overlap = both directions at
+        once / the slower alone for the kept pair (1.0 = fully concurrent)."""
+        o, n = C.c_double(), C.c_int()
+        check(self.lib.cloudsc_debug_host_pipeline_engine_check(self.h, C.byref(o), C.byref(n)))
+        return o.value, n.value
 
     def host_arrays(self):
         """(pointer, bytes) of every host array handed to the pipeline."""

@@ -67,6 +67,9 @@ int kseg_check(int device, void* stream, void* scratch);
 // workgroup-seconds behind it; reset zeroes the sums
 int kseg_clock(int device, void* stream, void* scratch, bool reset, double* ghz, double* seconds);
 
+// copy ceiling on the pipelines' engine pair (cloudsc_pipeline.hip)
+int pcie_engine_gbps(int device, size_t nb, int reps, double* h2d, double* d2h, double* both);
+
 }  // namespace cloudsc_impl
 
 #define HIPCHK(call)                                                \

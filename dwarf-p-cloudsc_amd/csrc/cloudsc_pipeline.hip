@@ -140,6 +140,9 @@ struct HsaEngines {
   bool ok = false;
   hsa_agent_t cpu{}, gpu{};
   hsa_amd_sdma_engine_id_t h2d{}, d2h{};
+  uint32_t rec_in = 0, rec_out = 0;    // the runtime's recommended engine masks per direction
+  double overlap = 0.0;                // both-at-once time / the slower direction alone (1 = full overlap)
+  int pairs_tried = 0;
 };
 
 struct AgentSearch {
@@ -191,11 +194,137 @@ HsaEngines find_engines(int device) {
   uint32_t out = pick_engine(rec_out ? rec_out : 0x6, in);
   if (!out) out = pick_engine(0xffff, in);
   if (!in || !out) return e;
+  e.rec_in = rec_in; e.rec_out = rec_out;
   e.cpu = q.cpu; e.gpu = q.gpu;
   e.h2d = (hsa_amd_sdma_engine_id_t)in;
   e.d2h = (hsa_amd_sdma_engine_id_t)out;
   e.ok = true;
   return e;
+}
+
+// Engine pair check at creation.  One diagnostic run of the engine path ran
+// every step with the two directions serialised (174 ms instead of 103 ms per
+// step, the same engine ids; profiles/r04/pipeline_steps_r04.jsonl), so the
+// pair is measured before it is used: 256 MiB H2D alone, D2H alone, then both
+// at once; overlap = both / the slower alone (1.0 when the directions run
+// fully concurrently, 2.0 when serialised).  Pairs from the recommended masks
+// first, then the other engines; the first pair below 1.3 is taken, else the
+// best one seen (at most kMaxPairs).
+constexpr int kMaxPairs = 6;
+double time_pair(const HsaEngines& e, hsa_amd_sdma_engine_id_t ein, hsa_amd_sdma_engine_id_t eout, char* h_in,
+                 char* h_out, char* d_in, char* d_out, size_t nb, hsa_signal_t sg, int dirs) {
+  const size_t piece = (size_t)64 << 20;
+  int n = 0;
+  for (size_t off = 0; off < nb; off += piece) n += ((dirs & 1) ? 1 : 0) + ((dirs & 2) ? 1 : 0);
+  hsa_signal_store_screlease(sg, n);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t off = 0; off < nb; off += piece) {
+    const size_t len = std::min(piece, nb - off);
+    if ((dirs & 1) && hsa_amd_memory_async_copy_on_engine(d_in + off, e.gpu, h_in + off, e.cpu, len, 0, nullptr, sg,
+                                                          ein, true) != HSA_STATUS_SUCCESS) {
+      hsa_signal_subtract_screlease(sg, 1);
+      return -1.0;
+    }
+    if ((dirs & 2) && hsa_amd_memory_async_copy_on_engine(h_out + off, e.cpu, d_out + off, e.gpu, len, 0, nullptr, sg,
+                                                          eout, true) != HSA_STATUS_SUCCESS) {
+      hsa_signal_subtract_screlease(sg, 1);
+      return -1.0;
+    }
+  }
+  if (hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) != 0) return -1.0;
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void check_engines(HsaEngines& e) {
+  const size_t nb = (size_t)256 << 20;
+  char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+  hsa_signal_t sg{};
+  bool have_sg = false;
+  if (hipHostMalloc((void**)&h_in, nb, hipHostMallocDefault) == hipSuccess &&
+      hipHostMalloc((void**)&h_out, nb, hipHostMallocDefault) == hipSuccess &&
+      hipMalloc((void**)&d_in, nb) == hipSuccess && hipMalloc((void**)&d_out, nb) == hipSuccess &&
+      hipMemset(d_out, 1, nb) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+      hsa_signal_create(0, 0, nullptr, &sg) == HSA_STATUS_SUCCESS) {
+    have_sg = true;
+    std::memset(h_in, 2, nb);
+    // candidate pairs: recommended engines first, then every other engine bit
+    std::vector<std::pair<uint32_t, uint32_t>> pairs;
+    const uint32_t rin = e.rec_in ? e.rec_in : 0x1, rout = e.rec_out ? e.rec_out : 0x6;
+    pairs.push_back({(uint32_t)e.h2d, (uint32_t)e.d2h});
+    for (uint32_t a = 1; a && a <= 0x8000; a <<= 1)
+      for (uint32_t b = 1; b && b <= 0x8000; b <<= 1) {
+        if (a == b) continue;
+        const int rank = ((rin & a) ? 0 : 1) + ((rout & b) ? 0 : 1);
+        if (rank == 0 && !(a == (uint32_t)e.h2d && b == (uint32_t)e.d2h)) pairs.push_back({a, b});
+      }
+    for (uint32_t b = 1; b && b <= 0x8000; b <<= 1)
+      if (b != (uint32_t)e.h2d && !(rout & b)) pairs.push_back({(uint32_t)e.h2d, b});
+    double best = 1e30;
+    std::pair<uint32_t, uint32_t> pick{(uint32_t)e.h2d, (uint32_t)e.d2h};
+    for (size_t i = 0; i < pairs.size() && e.pairs_tried < kMaxPairs; i++) {
+      const auto ein = (hsa_amd_sdma_engine_id_t)pairs[i].first, eout = (hsa_amd_sdma_engine_id_t)pairs[i].second;
+      if (time_pair(e, ein, eout, h_in, h_out, d_in, d_out, nb, sg, 3) < 0.0) continue;   // warm-up / unusable pair
+      const double ti = time_pair(e, ein, eout, h_in, h_out, d_in, d_out, nb, sg, 1);
+      const double to = time_pair(e, ein, eout, h_in, h_out, d_in, d_out, nb, sg, 2);
+      const double tb = time_pair(e, ein, eout, h_in, h_out, d_in, d_out, nb, sg, 3);
+      e.pairs_tried++;
+      if (ti <= 0.0 || to <= 0.0 || tb <= 0.0) continue;
+      const double r = tb / std::max(ti, to);
+      if (r < best) { best = r; pick = pairs[i]; }
+      if (r < 1.3) break;
+    }
+    if (best < 1e30) {
+      e.h2d = (hsa_amd_sdma_engine_id_t)pick.first;
+      e.d2h = (hsa_amd_sdma_engine_id_t)pick.second;
+      e.overlap = best;
+    }
+  }
+  if (have_sg) hsa_signal_destroy(sg);
+  if (d_in) (void)hipFree(d_in);
+  if (d_out) (void)hipFree(d_out);
+  if (h_in) (void)hipHostFree(h_in);
+  if (h_out) (void)hipHostFree(h_out);
+  (void)hipGetLastError();
+}
+
+// The copy ceiling on the engine pair the pipelines use (cloudsc_pcie_gbps
+// takes the better of this and its HIP-stream figures): H2D alone, D2H alone
+// and both at once of `nb` bytes each way, best of `reps`; 0 when the engines
+// are not available.
+int cloudsc_impl::pcie_engine_gbps(int device, size_t nb, int reps, double* h2d, double* d2h, double* both) {
+  *h2d = *d2h = *both = 0.0;
+  HsaEngines e = find_engines(device);
+  if (!e.ok) return CLOUDSC_OK;
+  check_engines(e);
+  char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+  hsa_signal_t sg{};
+  bool have_sg = false;
+  int rc = CLOUDSC_OK;
+  if (hipHostMalloc((void**)&h_in, nb, hipHostMallocDefault) == hipSuccess &&
+      hipHostMalloc((void**)&h_out, nb, hipHostMallocDefault) == hipSuccess &&
+      hipMalloc((void**)&d_in, nb) == hipSuccess && hipMalloc((void**)&d_out, nb) == hipSuccess &&
+      hipMemset(d_out, 1, nb) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+      hsa_signal_create(0, 0, nullptr, &sg) == HSA_STATUS_SUCCESS) {
+    have_sg = true;
+    std::memset(h_in, 2, nb);
+    double* out[3] = {h2d, d2h, both};
+    for (int dirs = 1; dirs <= 3; dirs++)
+      for (int r = -1; r < reps; r++) {
+        const double ms = time_pair(e, e.h2d, e.d2h, h_in, h_out, d_in, d_out, nb, sg, dirs);
+        if (ms <= 0.0) { rc = CLOUDSC_EHIP; break; }
+        const double gbs = (dirs == 3 ? 2.0 : 1.0) * (double)nb / (ms * 1e-3) / 1e9;
+        if (r >= 0 && gbs > *out[dirs - 1]) *out[dirs - 1] = gbs;
+      }
+  } else {
+    rc = CLOUDSC_ENOMEM;
+  }
+  if (have_sg) hsa_signal_destroy(sg);
+  if (d_in) (void)hipFree(d_in);
+  if (d_out) (void)hipFree(d_out);
+  if (h_in) (void)hipHostFree(h_in);
+  if (h_out) (void)hipHostFree(h_out);
+  (void)hipGetLastError();
+  return rc;
 }
 
 struct cloudsc_host_pipeline {
@@ -434,6 +563,7 @@ int cloudsc_host_pipeline_create(cloudsc_host_pipeline_t** out, int device, int 
   bool all_dev = true;
   for (int i = 0; i < kNumFields; i++) all_dev = all_dev && (!hf[i] || p->host_dev[i]);
   if (all_dev) p->eng = find_engines(device);
+  if (p->eng.ok) check_engines(p->eng);
   if (p->eng.ok) {
     for (auto* v : {&p->sig_in, &p->sig_out})
       for (size_t k = 0; k < p->slots.size(); k++) {
@@ -602,6 +732,13 @@ int cloudsc_debug_host_pipeline_copy(const cloudsc_host_pipeline_t* p, int* mode
   if (mode) *mode = p->eng.ok ? PC_ENGINES : PC_HIP;
   if (h2d_engine) *h2d_engine = p->eng.ok ? (int)p->eng.h2d : 0;
   if (d2h_engine) *d2h_engine = p->eng.ok ? (int)p->eng.d2h : 0;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_debug_host_pipeline_engine_check(const cloudsc_host_pipeline_t* p, double* overlap, int* pairs_tried) {
+  if (!p) return CLOUDSC_EINVAL;
+  if (overlap) *overlap = p->eng.ok ? p->eng.overlap : 0.0;
+  if (pairs_tried) *pairs_tried = p->eng.ok ? p->eng.pairs_tried : 0;
   return CLOUDSC_OK;
 }
 

@@ -473,6 +473,14 @@ int cloudsc_debug_set_pipeline_copy(int mode);
 int cloudsc_debug_host_pipeline_copy(const cloudsc_host_pipeline_t *pipe, int *mode, int *h2d_engine,
                                      int *d2h_engine);
 
+/* Diagnostic: the engine pair check a pipeline ran at creation (copy mode 1):
+ * *overlap = time of 256 MiB each way at once / the slower direction alone
+ * (1.0 = the directions fully concurrent, 2.0 = serialised) for the pair it
+ * kept, *pairs_tried = engine pairs measured (the first pair under 1.3 is
+ * kept, else the best of at most 6).  Both 0 in HIP-stream mode. */
+int cloudsc_debug_host_pipeline_engine_check(const cloudsc_host_pipeline_t *pipe, double *overlap,
+                                             int *pairs_tried);
+
 /* ------------------------------------------------------------------------ */
 /* One synchronous step on host arrays, callable from any host thread        */
 /* ------------------------------------------------------------------------ */

@@ -95,6 +95,7 @@ def run(kind, copy=1):
         hp.h = h
     try:
         mode, e_in, e_out = hp.copy_path()
+        overlap, pairs = hp.engine_check()
         nodes = host_nodes(hp.state.arrays)
         hp.run(ca.VARIANT_KSEG)
         ms = [round(hp.run(ca.VARIANT_KSEG), 2) for _ in range(steps)]
@@ -102,7 +103,8 @@ def run(kind, copy=1):
         hp.close()
         for p in keep:
             hip.hipHostFree(p)
-    print(json.dumps({"host_memory": kind, "copy": COPY[copy], "engines": [e_in, e_out],
+    print(json.dumps({"host_memory": kind, "copy": COPY[copy], "engines": [e_in, e_out], "engine_overlap": round(overlap, 3),
+                      "pairs_tried": pairs,
                       "host_numa_nodes": nodes, "gpu_numa_node": GPU_NODE,
                       "chunk_blocks": chunk, "slots": slots, "ms": ms,
                       "median": float(np.median(ms)), "min": min(ms)}), flush=True)
