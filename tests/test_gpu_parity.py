@@ -396,7 +396,8 @@ def test_host_pipeline_copy_paths(lib, ds, variant):
     engines pinned per direction -- the default --, HIP streams, HIP streams
     with a copy kernel for the outputs) gives the resident bits, over chunks
     whose slots are reused (7 chunks on 3 slots, the last one partial).  The
-    default path runs on two different engines."""
+    default path runs on two different engines, whose overlap it measured at
+    creation."""
     ref = run_gpu(ds, 1000, 64, variant=ca.VARIANT_KCACHE)
     assert lib.cloudsc_debug_set_pipeline_copy(3) == ca.EINVAL
     try:
@@ -407,6 +408,9 @@ def test_host_pipeline_copy_paths(lib, ds, variant):
                 m, e_in, e_out = hp.copy_path()
                 if mode == 1:
                     assert m == 1 and e_in and e_out and e_in != e_out, (m, e_in, e_out)
+                    # the engine pair check at creation measured the kept pair
+                    overlap, pairs = hp.engine_check()
+                    assert 1 <= pairs <= 6 and 0.5 < overlap < 2.5, (overlap, pairs)
                 hp.run(variant)
                 hp.run(variant)
                 out = hp.outputs()
