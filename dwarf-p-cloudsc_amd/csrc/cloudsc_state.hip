@@ -200,7 +200,10 @@ int field_alloc(cloudsc_gpu_state* s, Arena& ar, void** p, size_t bytes) {
 // only by those launches and are reset afterwards: the results do not depend
 // on it (cloudsc_debug_set_placement_search turns it off).
 std::atomic<int> g_place_passes{2};   // cloudsc_debug_set_placement_search
-constexpr int kPlaceSets = 4;         // whole fresh output sets tried before the field-by-field passes
+#ifndef CLOUDSC_PLACE_SETS   // experiment builds: make variant VFLAGS=-DCLOUDSC_PLACE_SETS=n
+#define CLOUDSC_PLACE_SETS 4
+#endif
+constexpr int kPlaceSets = CLOUDSC_PLACE_SETS;   // whole fresh output sets tried before the field-by-field passes
 
 // the KSEG kernel's time on the state's inputs with the output pointers of f:
 // best of 2 timed launches after one untimed, in ms; < 0 on an error
