@@ -201,7 +201,7 @@ int field_alloc(cloudsc_gpu_state* s, Arena& ar, void** p, size_t bytes) {
 // on it (cloudsc_debug_set_placement_search turns it off).
 std::atomic<int> g_place_passes{2};   // cloudsc_debug_set_placement_search
 #ifndef CLOUDSC_PLACE_SETS   // experiment builds: make variant VFLAGS=-DCLOUDSC_PLACE_SETS=n
-#define CLOUDSC_PLACE_SETS 4
+#define CLOUDSC_PLACE_SETS 8
 #endif
 constexpr int kPlaceSets = CLOUDSC_PLACE_SETS;   // whole fresh output sets tried before the field-by-field passes
 
@@ -249,29 +249,38 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
     return q;
   };
   int rc = CLOUDSC_OK;
-  // whole fresh output sets: even sets in field order, odd sets in a shuffled
-  // order with a spacer of 2-32 MiB before each field, so that the fields'
-  // relative physical placement differs from the first set's, not just its
-  // base (one searched state in six kept its slow time through two plain sets,
-  // profiles/r04/placement/placement_search_ab_fp64.jsonl).  The rejected sets
-  // and the spacers are freed when this phase ends.
-  std::vector<void*> set_held;
+  // whole fresh output sets: the first in field order, the others in a
+  // shuffled order with a spacer of 2-32 MiB before each field, so that the
+  // fields' relative physical placement changes, not just the set's base (with
+  // plain sets one searched state in six kept its slow time,
+  // profiles/r04/placement/placement_search_ab_fp64.jsonl).  A rejected set
+  // is freed at once (the spacers, held to the end of this phase, keep the next
+  // set off its pages), so the phase holds at most two output sets.
+  std::vector<void*> spacers;
   uint32_t rng = 0x9e3779b9u ^ (uint32_t)(uintptr_t)s;
   auto next = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
+  auto owned = [&](void* p) {
+    for (void* q : s->allocs)
+      if (q == p) return true;
+    return false;
+  };
+  auto release = [&](void* p) {     // the state's first allocation is held to the end (a timed-out search reverts)
+    if (owned(p)) held.push_back(p); else (void)hipFree(p);
+  };
   for (int k = 0; k < kPlaceSets && room && rc == CLOUDSC_OK; k++) {
     cloudsc_fields_t cand = best_f;
     void** cf = (void**)&cand;
     int order[64];
     for (int q = 0; q < n; q++) order[q] = q;
-    if (k & 1)
+    if (k > 0)
       for (int q = n - 1; q > 0; q--) std::swap(order[q], order[next() % (q + 1)]);
     int got = 0;
     for (int i = 0; i < n; i++) {
       const int q = order[i];
-      if (k & 1) {
+      if (k > 0) {
         void* sp = fresh(((size_t)1 + next() % 16) << 21);
         if (!sp) break;
-        set_held.push_back(sp);
+        spacers.push_back(sp);
       }
       void* p = fresh(bytes[q]);
       if (!p) break;
@@ -284,21 +293,15 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
     }
     const float t = probe_kernel(s, cand);
     s->place_tries += n;
-    if (t < 0.f) { rc = CLOUDSC_EHIP; for (int q = 0; q < n; q++) set_held.push_back(cf[members[q]]); break; }
+    if (t < 0.f) { rc = CLOUDSC_EHIP; for (int q = 0; q < n; q++) (void)hipFree(cf[members[q]]); break; }
     if (t < best * 0.99f) {
-      for (int q = 0; q < n; q++) set_held.push_back(bf[members[q]]);
+      for (int q = 0; q < n; q++) release(bf[members[q]]);
       best_f = cand; best = t; s->place_moves += n;
     } else {
-      for (int q = 0; q < n; q++) set_held.push_back(cf[members[q]]);
+      for (int q = 0; q < n; q++) (void)hipFree(cf[members[q]]);
     }
   }
-  // candidates and spacers are freed now; a replaced first allocation (owned
-  // by the state) is held to the end, where a timed-out search reverts to it
-  for (void* p : set_held) {
-    bool owned = false;
-    for (void* q : s->allocs) owned = owned || q == p;
-    if (owned) held.push_back(p); else (void)hipFree(p);
-  }
+  for (void* p : spacers) (void)hipFree(p);
   room = true;
   // one field at a time
   for (int pass = 0; pass < passes && room && rc == CLOUDSC_OK; pass++) {
