@@ -328,15 +328,6 @@ template <typename real> constexpr int kKsegSplitPct = CLOUDSC_KSEG_SPLIT_PCT;
 #else
 template <typename real> constexpr int kKsegSplitPct = sizeof(real) == 8 ? 55 : 50;
 #endif
-// Tail split (PersistArgs::ntail): the share of each stripe's blocks whose last
-// segment runs as two items, the second ones dequeued last, and where their
-// last segment is cut (per cent of its levels).  0 = off.
-#ifndef CLOUDSC_KSEG_TAIL_PCT
-#define CLOUDSC_KSEG_TAIL_PCT 0
-#endif
-#ifndef CLOUDSC_KSEG_TAIL_CUT_PCT
-#define CLOUDSC_KSEG_TAIL_CUT_PCT 50
-#endif
 
 void kseg_bounds(int nseg, int klev, int ncldtop, int split_pct, int* lev) {
   const int top = ncldtop - 1 < klev ? (ncldtop - 1 > 0 ? ncldtop - 1 : 0) : klev;
@@ -411,8 +402,7 @@ int launch_kseg_cfg(hipStream_t st, const KArgs<real>& a, const PersistArgs<real
     ncu = 256;
   constexpr int kSimdsPerCu = 4;                       // CDNA4 compute unit
   const int simds = kSimdsPerCu * ncu;
-  (void)nitems; (void)nseg;
-  const int units = pa.nblocks * pa.nsub;              // 64-column sub-blocks
+  const int units = nitems / (nseg > 0 ? nseg : 1);   // 64-column sub-blocks
   const int per_simd = per_cu / kSimdsPerCu > 0 ? per_cu / kSimdsPerCu : 1;
   int w = units / simds;
   if (w < 1) w = 1;
@@ -511,18 +501,6 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
       pa.lev[n] = klev;
     }
 #endif
-    pa.ntail = 0;
-    pa.levmid = pa.lev[pa.nseg];
-    {
-      const int l0 = pa.lev[pa.nseg - 1], l1 = pa.lev[pa.nseg];
-      const int cut = l0 + (int)(((long long)(l1 - l0) * CLOUDSC_KSEG_TAIL_CUT_PCT + 50) / 100);
-      if (CLOUDSC_KSEG_TAIL_PCT > 0 && cut > l0 && cut < l1) {
-        // per stripe: the last CLOUDSC_KSEG_TAIL_PCT % of its blocks (nbs of the first stripe; a smaller stripe takes min)
-        const int nbs0 = (nblocks + kKsegStripes - 1) / kKsegStripes;
-        pa.ntail = (nbs0 * CLOUDSC_KSEG_TAIL_PCT + 50) / 100;
-        pa.levmid = cut;
-      }
-    }
     pa.nitems = pa.nseg * nblocks * pa.nsub;
     const bool zero_ws = !(ep && ep->ready);
     if (zero_ws) {
@@ -547,8 +525,7 @@ int launch_v(hipStream_t st, int variant, const cloudsc_fields_t* f, int ngptot,
       for (int q = 0; q < kKsegStripes; q++) {
         const unsigned nbs = q < S ? (unsigned)((nblocks - q + S - 1) / S) : 0u;
         const unsigned wgs = q < S ? (unsigned)((grid - q + S - 1) / S) : 0u;
-        const unsigned ntl = (unsigned)pa.ntail < nbs ? (unsigned)pa.ntail : nbs;
-        ep->base[q] = pa.base[q] + ((unsigned)pa.nseg * nbs + ntl) * (unsigned)pa.nsub + wgs;
+        ep->base[q] = pa.base[q] + (unsigned)pa.nseg * nbs * (unsigned)pa.nsub + wgs;
       }
       ep->stamp = pa.stamp + (unsigned)(kMaxSeg + 1);
       ep->ready = true;

@@ -1360,11 +1360,6 @@ struct PersistArgs {
   // effective shader clock of the launches (cloudsc_state_kseg_clock)
   unsigned long long* clk;
   int lev[kMaxSeg + 1];
-  // tail split: in every stripe the last `ntail` blocks (lb >= nbs - ntail)
-  // run their last segment as two items, [lev[nseg-1], levmid) in the normal
-  // order and [levmid, lev[nseg]) after every other item of the stripe, so the
-  // items dequeued last are half as long (0 = off)
-  int ntail, levmid;
 };
 
 // write-through (sc1) store of a handed-off value: an agent-scope relaxed atomic
@@ -1414,9 +1409,7 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
   const int st = (int)(blockIdx.x % (unsigned)S);
   const int nbs = (P.nblocks - st + S - 1) / S;
   const int nsbs = nbs * nsub;                        // items per segment in the stripe
-  const int ntl = P.ntail < nbs ? P.ntail : nbs;     // tail-split blocks of the stripe
-  const int main_items = P.nseg * nsbs;
-  const int items = main_items + ntl * nsub;
+  const int items = P.nseg * nsbs;
   unsigned* const ctr = P.ctr + st * kKsegCtrStride;
   const unsigned base = P.base[st];
   for (;;) {
@@ -1432,16 +1425,9 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
     // (or (segment, h, lb) with sb_major): a block of NPROMA > 64 columns is run
     // as nsub one-wave items over the same block layout (sub-block h is the 64
     // contiguous columns h*64.. of each plane); flags are per (b, h)
-    // (the tail split's second halves come after every other item: segment
-    // index nseg, waiting for the first half's flag, stamp + nseg)
-    const bool second = item >= main_items;
-    const int seg = second ? P.nseg : item / nsbs, r = second ? item - main_items : item - seg * nsbs;
-    const int lb = second ? nbs - ntl + r / nsub : (P.sb_major ? r % nbs : r / nsub);
-    const int hh = second ? r % nsub : (P.sb_major ? r / nbs : r - lb * nsub);
-    const bool split_first = !second && seg == P.nseg - 1 && lb >= nbs - ntl;
-    const int lev0 = second ? P.levmid : P.lev[seg];
-    const int lev1 = split_first ? P.levmid : P.lev[second ? P.nseg : seg + 1];
-    const bool last = second || (seg == P.nseg - 1 && !split_first);
+    const int seg = item / nsbs, r = item - seg * nsbs;
+    const int lb = P.sb_major ? r % nbs : r / nsub;
+    const int hh = P.sb_major ? r / nbs : r - lb * nsub;
     const int b = lb * S + st;
     const int sb = b * nsub + hh;
     const int jl = hh * 64 + (int)threadIdx.x;
@@ -1482,8 +1468,8 @@ __device__ __forceinline__ void cloudsc_kcache_persistent_body(cptr<KArgs<real>>
 #endif
       if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, false);
     }
-    if (active) kcache_levels<real, PF, AER>(ka, cpar, b, lo, lev0, lev1, cs);
-    if (!last) {
+    if (active) kcache_levels<real, PF, AER>(ka, cpar, b, lo, P.lev[seg], P.lev[seg + 1], cs);
+    if (seg + 1 < P.nseg) {
       // producer (G16 R1): sc1 payload stores, every wave drains, barrier, the
       // flag stored with an agent atomic
       if (active) carry_io(P.state, ust, (size_t)nproma, lo, cs, true);
