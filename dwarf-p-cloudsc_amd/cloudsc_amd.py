@@ -404,6 +404,7 @@ def gpu_lib(path: Optional[str] = None):
                                                          C.POINTER(C.c_int)]
         lib.cloudsc_debug_host_pipeline_engine_check.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                                                  C.POINTER(C.c_int)]
+        lib.cloudsc_host_pipeline_copy_bound.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     lib.cloudsc_gpu_init.argtypes = [C.c_int, C.POINTER(Params)]
     lib.cloudsc_gpu_run.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.POINTER(Fields), C.c_void_p]
@@ -686,6 +687,14 @@ class HostPipeline:
         m, a, b = C.c_int(), C.c_int(), C.c_int()
         check(self.lib.cloudsc_debug_host_pipeline_copy(self.h, C.byref(m), C.byref(a), C.byref(b)))
         return m.value, a.value, b.value
+
+    def copy_bound(self) -> float:
+        """ms of one step's copies without the kernels, same engines and
+        arrays (cloudsc_host_pipeline_copy_bound); clobbers the host outputs
+        and plude (restored by the next run())."""
+        t = C.c_double()
+        check(self.lib.cloudsc_host_pipeline_copy_bound(self.h, C.byref(t)))
+        return t.value
 
     def engine_check(self):
         """(overlap, pairs tried) of the engine pair check at creation

@@ -505,6 +505,68 @@ int run_on_engines(cloudsc_host_pipeline* p, int variant, int vk, double* ms) {
   return CLOUDSC_OK;
 }
 
+// one step's copies without the kernels, on the same engines, host arrays and
+// device slots: every input chunk H2D and every output chunk D2H, each
+// direction queued back to back on its engine (a slot's signals are reused
+// once its previous copies are done).  The bound the pipeline is held against:
+// the same bytes over the same path.  The outputs copied back are the slots'
+// contents, not results.
+int copies_only_on_engines(cloudsc_host_pipeline* p, double* ms) {
+  const int nchunks = (p->nblocks + p->chunk_blocks - 1) / p->chunk_blocks;
+  const int nslots = (int)p->slots.size();
+  const void* const* hf = (const void* const*)&p->host;
+  HIPCHK(hipDeviceSynchronize());
+  auto wait = [](hsa_signal_t sg) {
+    return hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) == 0
+               ? CLOUDSC_OK : CLOUDSC_EHIP;
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = CLOUDSC_OK;
+  for (int c = 0; c < nchunks && rc == CLOUDSC_OK; c++) {
+    auto& s = p->slots[c % nslots];
+    if (c >= nslots && ((rc = wait(p->sig_in[c % nslots])) || (rc = wait(p->sig_out[c % nslots])))) break;
+    const int b0 = c * p->chunk_blocks;
+    const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
+    void* const* df = (void* const*)&s.dev;
+    for (int in = 1; in >= 0 && rc == CLOUDSC_OK; in--) {
+      hsa_signal_t sg = in ? p->sig_in[c % nslots] : p->sig_out[c % nslots];
+      int n = 0;
+      for (int i = 0; i < kNumFields; i++) {
+        const int dir = kFieldTable[i].dir;
+        if (hf[i] && (in ? dir != FD_OUT : (dir == FD_OUT || dir == FD_INOUT))) n++;
+      }
+      hsa_signal_store_screlease(sg, n);
+      for (int i = 0; i < kNumFields; i++) {
+        const FieldDesc& d = kFieldTable[i];
+        if (!hf[i] || !(in ? d.dir != FD_OUT : (d.dir == FD_OUT || d.dir == FD_INOUT))) continue;
+        const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * (d.is_int ? sizeof(int) : p->es);
+        char* h = (char*)p->host_dev[i] + (size_t)b0 * per;
+        const hsa_status_t st =
+            in ? hsa_amd_memory_async_copy_on_engine(df[i], p->eng.gpu, h, p->eng.cpu, (size_t)nb * per, 0, nullptr,
+                                                     sg, p->eng.h2d, true)
+               : hsa_amd_memory_async_copy_on_engine(h, p->eng.cpu, df[i], p->eng.gpu, (size_t)nb * per, 0, nullptr,
+                                                     sg, p->eng.d2h, true);
+        if (st != HSA_STATUS_SUCCESS) {
+          hsa_signal_subtract_screlease(sg, n);
+          set_error_text("host pipeline: hsa_amd_memory_async_copy_on_engine failed");
+          rc = CLOUDSC_EHIP;
+          break;
+        }
+        n--;
+      }
+    }
+  }
+  for (auto* v : {&p->sig_in, &p->sig_out})
+    for (hsa_signal_t sg : *v) {
+      const int r = wait(sg);
+      if (r && !rc) rc = r;
+    }
+  const auto t1 = std::chrono::steady_clock::now();
+  if (rc) return rc;
+  if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  return CLOUDSC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -733,6 +795,13 @@ int cloudsc_debug_host_pipeline_copy(const cloudsc_host_pipeline_t* p, int* mode
   if (h2d_engine) *h2d_engine = p->eng.ok ? (int)p->eng.h2d : 0;
   if (d2h_engine) *d2h_engine = p->eng.ok ? (int)p->eng.d2h : 0;
   return CLOUDSC_OK;
+}
+
+int cloudsc_host_pipeline_copy_bound(cloudsc_host_pipeline_t* p, double* ms) {
+  if (!p || !ms) return CLOUDSC_EINVAL;
+  if (!p->eng.ok) return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(p->device));
+  return copies_only_on_engines(p, ms);
 }
 
 int cloudsc_debug_host_pipeline_engine_check(const cloudsc_host_pipeline_t* p, double* overlap, int* pairs_tried) {

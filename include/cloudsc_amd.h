@@ -473,6 +473,15 @@ int cloudsc_debug_set_pipeline_copy(int mode);
 int cloudsc_debug_host_pipeline_copy(const cloudsc_host_pipeline_t *pipe, int *mode, int *h2d_engine,
                                      int *d2h_engine);
 
+/* Measurement: the time of one step's copies WITHOUT the kernels, on the same
+ * copy engines, host arrays and device slots (every input H2D, every output
+ * D2H, each direction back to back on its engine): the bound a step of this
+ * pipeline is held against (bench.py's pcie_inclusive.bound_ms).  The host
+ * OUTPUT arrays and plude receive the device slots' contents, not results:
+ * run a step (with plude restored) before reading outputs again.
+ * CLOUDSC_EINVAL when the pipeline has no copy engines (HIP-stream mode). */
+int cloudsc_host_pipeline_copy_bound(cloudsc_host_pipeline_t *pipe, double *ms);
+
 /* Diagnostic: the engine pair check a pipeline ran at creation (copy mode 1):
  * *overlap = time of 256 MiB each way at once / the slower direction alone
  * (1.0 = the directions fully concurrent, 2.0 = serialised) for the pair it

@@ -411,6 +411,8 @@ def test_host_pipeline_copy_paths(lib, ds, variant):
                     # the engine pair check at creation measured the kept pair
                     overlap, pairs = hp.engine_check()
                     assert 1 <= pairs <= 6 and 0.5 < overlap < 2.5, (overlap, pairs)
+                    # the copies-only bound runs on the same arrays; the steps below restore plude
+                    assert hp.copy_bound() > 0.0
                 hp.run(variant)
                 hp.run(variant)
                 out = hp.outputs()
