@@ -148,6 +148,25 @@ def roofline_traffic(ca, path, key):
         entry["kernel_source_hash"])
 
 
+def box_info():
+    """The box's GPU memory / compute partition modes and memory clock range
+    (rocm-smi queries, read-only; best effort): boxes of the pool run the same
+    kernel at different speeds with a normal shader clock and STREAM rate
+    (DESIGN.md section 7), and these are the first settings that could tell them apart."""
+    import subprocess
+    out = {}
+    for key, flag in (("memory_partition", "--showmemorypartition"), ("compute_partition", "--showcomputepartition"),
+                      ("mclk_range", "--showmclkrange")):
+        try:
+            r = subprocess.run(["rocm-smi", flag, "--json"], capture_output=True, text=True, timeout=20)
+            d = json.loads(r.stdout) if r.returncode == 0 else {}
+            cards = sorted(k for k in d if k.startswith("card"))
+            out[key] = d[cards[0]] if cards else None
+        except (OSError, ValueError, subprocess.SubprocessError):
+            out[key] = None
+    return out
+
+
 def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
     """Host-resident block-layout arrays (pinned in place), per chunk H2D ->
     kernel -> D2H pipelined over the two directions' copy engines and a kernel stream: the
@@ -307,6 +326,7 @@ def main():
         "sclk_ghz": round(sclk, 4) if sclk else None,
         "sclk_method": "effective shader clock of the timed launches: each workgroup's s_memtime cycles over its "
                        "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",
+        "box": box_info() if rank == 0 else None,
         "placement": dict(per_rank[0]["placement"], method=(
             "output placement search at state creation (cloudsc_state_placement): the KSEG kernel on the state's "
             "own inputs timed (best of 2) over candidate placements -- whole fresh output sets, one output field at "
