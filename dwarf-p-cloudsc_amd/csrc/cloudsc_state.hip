@@ -356,52 +356,6 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
   return rc;
 }
 
-// Fresh KSEG workspaces (counters, flags and the carried state handed between
-// segments, written and read by every item), each after a spacer of 2-32 MiB:
-// the one allocation every input and output candidate shares.  A candidate is
-// zeroed like the first one and runs with a fresh epoch; it is kept when the
-// kernel is more than 1 % faster (and its launches report no timed-out
-// hand-off), else freed and the first workspace's epoch restored.
-constexpr int kPlaceWorkspaces = 4;
-int place_workspace(cloudsc_gpu_state* s, size_t wsb) {
-  float best = s->place_final_ms;
-  if (!(best > 0.f) || g_place_passes.load() <= 0) return CLOUDSC_OK;
-  std::vector<void*> spacers;
-  uint32_t rng = 0x7f4a7c15u ^ (uint32_t)(uintptr_t)s;
-  int rc = CLOUDSC_OK;
-  for (int k = 0; k < kPlaceWorkspaces && rc == CLOUDSC_OK; k++) {
-    rng = rng * 1664525u + 1013904223u;
-    void* sp = nullptr;
-    if (hipMalloc(&sp, ((size_t)1 + (rng >> 8) % 16) << 21) != hipSuccess) { (void)hipGetLastError(); break; }
-    spacers.push_back(sp);
-    void* ws = nullptr;
-    if (hipMalloc(&ws, wsb) != hipSuccess) { (void)hipGetLastError(); break; }
-    if (hipMemsetAsync(ws, 0, 256, s->stream) != hipSuccess) { (void)hipFree(ws); rc = CLOUDSC_EHIP; break; }
-    void* const old_ws = s->kseg_ws;
-    const cloudsc_impl::KsegEpoch old_ep = s->kseg_epoch;
-    s->kseg_ws = ws;
-    s->kseg_epoch = cloudsc_impl::KsegEpoch{};
-    const float t = probe_kernel(s, s->f);
-    s->place_tries++;
-    const int hc = t < 0.f ? CLOUDSC_EHIP : kseg_check(s->device, s->stream, ws);
-    if (hc == CLOUDSC_OK && t < best * 0.99f) {
-      best = t;
-      s->place_moves++;
-      s->allocs.push_back(ws);
-      dfree(s, old_ws);
-    } else {
-      s->kseg_ws = old_ws;
-      s->kseg_epoch = old_ep;
-      (void)hipStreamSynchronize(s->stream);
-      (void)hipFree(ws);
-      if (hc != CLOUDSC_OK && hc != CLOUDSC_EHANDOFF) rc = hc;
-    }
-  }
-  for (void* p : spacers) (void)hipFree(p);
-  if (rc == CLOUDSC_OK) s->place_final_ms = best;
-  return rc;
-}
-
 // Whole fresh INPUT sets, contents copied, after the output search: one state in
 // six kept its slow time through every output candidate
 // (profiles/r04/placement/placement_search_ab_fp64.jsonl), so the pages its
@@ -608,7 +562,6 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
       ibytes[nin++] = in.bytes;
     }
     if ((rc = place_inputs(s, imem, ibytes, nin))) return fail(rc);
-    if ((rc = place_workspace(s, (size_t)wsb))) return fail(rc);
   }
   for (Out& o : outs)
     if (hipMemsetAsync(*o.dst, 0xff, o.bytes, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);  // NaN
