@@ -363,7 +363,7 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
 // more than 1 % faster.  members/bytes: the input fields (positions in
 // cloudsc_fields_t); member -1 is the pristine plude copy.  Rejected sets are
 // held until the end, so a retry does not get the same pages back.
-constexpr int kPlaceInputSets = 2;
+constexpr int kPlaceInputSets = 4;   // the first in field order, the others shuffled with spacers
 int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, int n) {
   float best = s->place_final_ms;
   if (!(best > 0.f) || g_place_passes.load() <= 0) return CLOUDSC_OK;
@@ -372,13 +372,26 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
   cloudsc_fields_t best_f = s->f;
   void* best_pl = s->plude_pristine;
   std::vector<void*> mine;               // every candidate buffer allocated here
+  std::vector<void*> spacers;
+  uint32_t rng = 0x85ebca6bu ^ (uint32_t)(uintptr_t)s;
+  auto next = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
   int rc = CLOUDSC_OK;
   for (int k = 0; k < kPlaceInputSets && rc == CLOUDSC_OK; k++) {
     cloudsc_fields_t cand = s->f;
     void* cand_pl = s->plude_pristine;
     void** cf = (void**)&cand;
+    int order[64];
+    for (int q = 0; q < n; q++) order[q] = q;
+    if (k > 0)
+      for (int q = n - 1; q > 0; q--) std::swap(order[q], order[next() % (q + 1)]);
     int got = 0;
-    for (int q = 0; q < n; q++) {
+    for (int i = 0; i < n; i++) {
+      const int q = order[i];
+      if (k > 0) {
+        void* sp = nullptr;
+        if (hipMalloc(&sp, ((size_t)1 + next() % 16) << 21) != hipSuccess) { (void)hipGetLastError(); break; }
+        spacers.push_back(sp);
+      }
       void* p = nullptr;
       if (hipMalloc(&p, bytes[q]) != hipSuccess) { (void)hipGetLastError(); break; }
       mine.push_back(p);
@@ -397,6 +410,7 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
     if (t < best * 0.99f) { best = t; best_f = cand; best_pl = cand_pl; s->place_moves += n; }
   }
   if (hipStreamSynchronize(s->stream) != hipSuccess && rc == CLOUDSC_OK) rc = CLOUDSC_EHIP;
+  for (void* p : spacers) (void)hipFree(p);
   // as for the outputs: hand-off timeouts in the probes keep the first placement
   if (rc == CLOUDSC_OK) {
     const int hc = kseg_check(s->device, s->stream, s->kseg_ws);
