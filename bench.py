@@ -330,7 +330,7 @@ def main():
         "placement": dict(per_rank[0]["placement"], method=(
             "output placement search at state creation (cloudsc_state_placement): the KSEG kernel on the state's "
             "own inputs timed (best of 2) over candidate placements -- whole fresh output sets, one output field at "
-            "a time, then whole fresh input sets -- a candidate kept when it is > 1 % faster; probe ms of the "
+            "a time, then whole fresh input sets (the output and input sets after the first shuffled, with spacers) -- a candidate kept when it is > 1 % faster; probe ms of the "
             "first and the kept "
             "placement; rank 0")),
         "per_rank": per_rank,
