@@ -420,22 +420,35 @@ int run_on_engines(cloudsc_host_pipeline* p, int variant, int vk, double* ms) {
   const void* const* hf = (const void* const*)&p->host;
   HIPCHK(hipDeviceSynchronize());
   const auto t0 = std::chrono::steady_clock::now();
-  // the copies of chunk c in one direction, counted down on the slot's signal
-  auto issue = [&](int c, bool in) -> int {
+  // the copies of chunk c in one direction, counted down on the slot's signal.
+  // H2D is issued in two parts: part 0 sets the count for every H2D copy of
+  // the chunk and issues the pure inputs, part 1 issues the INOUT field
+  // (plude), which the slot's previous D2H still reads (the caller
+  // waits for that D2H between the two parts).  D2H is one part.
+  auto issue = [&](int c, bool in, int part) -> int {
     auto& s = p->slots[c % nslots];
     hsa_signal_t sg = in ? p->sig_in[c % nslots] : p->sig_out[c % nslots];
     const int b0 = c * p->chunk_blocks;
     const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
     void* const* df = (void* const*)&s.dev;
-    int n = 0;
-    for (int i = 0; i < kNumFields; i++) {
-      const int dir = kFieldTable[i].dir;
-      if (hf[i] && (in ? dir != FD_OUT : (dir == FD_OUT || dir == FD_INOUT))) n++;
+    auto selected = [&](int dir, int pt) {
+      if (!in) return dir == FD_OUT || dir == FD_INOUT;
+      return dir != FD_OUT && (pt < 0 || (pt == 0) == (dir != FD_INOUT));
+    };
+    int n = 0;                 // copies of this call not yet issued
+    for (int i = 0; i < kNumFields; i++)
+      if (hf[i] && selected(kFieldTable[i].dir, part)) n++;
+    int later = 0;             // part 1's copies, counted by part 0
+    if (part <= 0) {
+      int total = 0;
+      for (int i = 0; i < kNumFields; i++)
+        if (hf[i] && selected(kFieldTable[i].dir, -1)) total++;
+      later = total - n;
+      hsa_signal_store_screlease(sg, total);
     }
-    hsa_signal_store_screlease(sg, n);
     for (int i = 0; i < kNumFields; i++) {
       const FieldDesc& d = kFieldTable[i];
-      if (!hf[i] || !(in ? d.dir != FD_OUT : (d.dir == FD_OUT || d.dir == FD_INOUT))) continue;
+      if (!hf[i] || !selected(d.dir, part)) continue;
       const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * (d.is_int ? sizeof(int) : p->es);
       char* h = (char*)p->host_dev[i] + (size_t)b0 * per;
       const hsa_status_t st =
@@ -444,7 +457,7 @@ int run_on_engines(cloudsc_host_pipeline* p, int variant, int vk, double* ms) {
              : hsa_amd_memory_async_copy_on_engine(h, p->eng.cpu, df[i], p->eng.gpu, (size_t)nb * per, 0, nullptr, sg,
                                                    p->eng.d2h, true);
       if (st != HSA_STATUS_SUCCESS) {
-        hsa_signal_subtract_screlease(sg, n);   // the copies not issued (the issued ones still count down)
+        hsa_signal_subtract_screlease(sg, n + later);   // the copies not issued (the issued ones still count down)
         set_error_text("host pipeline: hsa_amd_memory_async_copy_on_engine failed");
         return CLOUDSC_EHIP;
       }
@@ -458,20 +471,30 @@ int run_on_engines(cloudsc_host_pipeline* p, int variant, int vk, double* ms) {
                ? CLOUDSC_OK : CLOUDSC_EHIP;
   };
   int rc = CLOUDSC_OK;
+  int out_issued = -1;                     // the last chunk whose D2H is issued
+  // a chunk's outputs (and plude), once its kernel is done
+  auto drain = [&](int c) -> int {
+    if (hipEventSynchronize(p->slots[c % nslots].k_done) != hipSuccess) return CLOUDSC_EHIP;
+    out_issued = c;
+    return issue(c, false, 0);
+  };
   for (int c = 0; c < nchunks && rc == CLOUDSC_OK; c++) {
     auto& s = p->slots[c % nslots];
     const bool reuse = c >= nslots;        // the slot held chunk c - nslots
     // inputs: after the slot's previous kernel has read its inputs
     if (reuse && hipEventSynchronize(s.k_done) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
-    if ((rc = issue(c, true))) break;
-    // the previous chunk's outputs, as soon as its kernel is done
-    if (c >= 1) {
-      if (hipEventSynchronize(p->slots[(c - 1) % nslots].k_done) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
-      if ((rc = issue(c - 1, false))) break;
+    if ((rc = issue(c, true, 0))) break;
+    // plude: after the slot's previous D2H has read it back (with one slot
+    // that D2H is the previous chunk's, not issued yet)
+    if (reuse) {
+      if (out_issued < c - nslots && (rc = drain(c - nslots))) break;
+      if ((rc = wait(p->sig_out[c % nslots]))) break;
     }
+    if ((rc = issue(c, true, 1))) break;
+    // the previous chunk's outputs, as soon as its kernel is done
+    if (c >= 1 && out_issued < c - 1 && (rc = drain(c - 1))) break;
     // kernel: after its inputs are in and the slot's previous outputs are out
     if ((rc = wait(p->sig_in[c % nslots]))) break;
-    if (reuse && (rc = wait(p->sig_out[c % nslots]))) break;
     const int b0 = c * p->chunk_blocks;
     const int nb = (b0 + p->chunk_blocks <= p->nblocks) ? p->chunk_blocks : p->nblocks - b0;
     const long long col0 = (long long)b0 * p->nproma;
@@ -482,10 +505,7 @@ int run_on_engines(cloudsc_host_pipeline* p, int variant, int vk, double* ms) {
       break;
     if (hipEventRecord(s.k_done, p->st_k) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
   }
-  if (rc == CLOUDSC_OK) {
-    if (hipEventSynchronize(p->slots[(nchunks - 1) % nslots].k_done) != hipSuccess) rc = CLOUDSC_EHIP;
-    else rc = issue(nchunks - 1, false);
-  }
+  if (rc == CLOUDSC_OK && out_issued < nchunks - 1) rc = drain(nchunks - 1);
   // every copy issued, finished (also after a failure: the slots are reused)
   for (auto* v : {&p->sig_in, &p->sig_out})
     for (hsa_signal_t sg : *v) {
@@ -656,6 +676,9 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
       void* q = nullptr;
       if (hipMalloc(&q, (size_t)nb) != hipSuccess) return CLOUDSC_ENOMEM;
       p->allocs.push_back(q);
+      // control words of a fresh KSEG workspace (recycled memory may hold a
+      // matching tag and a stale hand-off error count)
+      if (hipMemset(q, 0, 256) != hipSuccess) return CLOUDSC_EHIP;
       s.scratch = q;
       s.scratch_bytes = (size_t)nb;
     }
@@ -677,15 +700,19 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
     const int ncols = (int)((col0 + (long long)nb * p->nproma <= p->ngptot) ? (long long)nb * p->nproma
                                                                             : p->ngptot - col0);
     void* const* df = (void* const*)&s.dev;
-    // inputs: after the slot's previous kernel has read its inputs
+    // inputs: after the slot's previous kernel has read its inputs; plude
+    // (INOUT) last, after the slot's previous D2H has read it back
     if (reuse) HIPCHK(hipStreamWaitEvent(p->st_in, s.k_done, 0));
-    for (int i = 0; i < kNumFields; i++) {
-      const FieldDesc& d = kFieldTable[i];
-      if (!hf[i] || d.dir == FD_OUT) continue;
-      const size_t eb = d.is_int ? sizeof(int) : p->es;
-      const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * eb;
-      HIPCHK(hipMemcpyAsync(df[i], (const char*)hf[i] + (size_t)b0 * per, (size_t)nb * per, hipMemcpyHostToDevice,
-                            p->st_in));
+    for (int part = 0; part < 2; part++) {
+      if (part == 1 && reuse) HIPCHK(hipStreamWaitEvent(p->st_in, s.out_done, 0));
+      for (int i = 0; i < kNumFields; i++) {
+        const FieldDesc& d = kFieldTable[i];
+        if (!hf[i] || d.dir == FD_OUT || (part == 0) != (d.dir != FD_INOUT)) continue;
+        const size_t eb = d.is_int ? sizeof(int) : p->es;
+        const size_t per = per_block_elems(d.kind, p->nproma, p->klev) * eb;
+        HIPCHK(hipMemcpyAsync(df[i], (const char*)hf[i] + (size_t)b0 * per, (size_t)nb * per, hipMemcpyHostToDevice,
+                              p->st_in));
+      }
     }
     HIPCHK(hipEventRecord(s.in_done, p->st_in));
     // kernel: after its inputs are in and the slot's previous outputs are out
@@ -946,6 +973,7 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
       const hipError_t e = hipMalloc(&ctx->scratch, (size_t)nb);
       if (e != hipSuccess) { ctx->scratch = nullptr; hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
       ctx->scratch_bytes = (size_t)nb;
+      HIPCHK(hipMemsetAsync(ctx->scratch, 0, 256, ctx->st));   // control words (recycled memory)
     }
   }
   rc = gpu_run_impl(device, ctx->st, precision, variant, ngptot, nproma, klev, &dev, ctx->scratch, nullptr,

@@ -147,9 +147,19 @@ def test_scc_private_equals_kcache_bitwise(lib, ds, precision):
         assert np.array_equal(a[k], b[k]), k
 
 
+def gpu_init_default(lib, ds, device=0):
+    """cloudsc_gpu_init: the device's default parameter set, which the
+    low-level cloudsc_gpu_run reads (each test sets it itself, so it passes
+    alone)."""
+    import ctypes as C
+    prm = ca.Params.from_dict(ds.params)
+    ca.check(lib.cloudsc_gpu_init(device, C.byref(prm)))
+
+
 def test_scc_private_klev_bound(lib, ds):
     """The private arrays are sized for the reference's klev = 137: more levels is EINVAL."""
     import ctypes as C
+    gpu_init_default(lib, ds)
     g = ca.GpuState(ds, 256, 128)
     try:
         f = ca.Fields()
@@ -229,6 +239,7 @@ def test_full_size_validation(lib, ds):
 def test_low_level_run_entry(lib, ds):
     """cloudsc_gpu_run on caller-owned device buffers (the drop-in boundary)."""
     import ctypes as C
+    gpu_init_default(lib, ds)
     g = ca.GpuState(ds, 256, 128)
     try:
         f = ca.Fields()
@@ -390,20 +401,23 @@ def test_host_pipeline_fp32(lib, ds):
         assert np.array_equal(out[k], ref[k]), k
 
 
-@pytest.mark.parametrize("variant", [ca.VARIANT_KSEG, ca.VARIANT_KCACHE])
-def test_host_pipeline_copy_paths(lib, ds, variant):
+@pytest.mark.parametrize("variant,nstreams", [(ca.VARIANT_KSEG, 3), (ca.VARIANT_KCACHE, 3), (ca.VARIANT_KSEG, 1),
+                                              (ca.VARIANT_KCACHE, 2)])
+def test_host_pipeline_copy_paths(lib, ds, variant, nstreams):
     """Every copy path of the pipeline (cloudsc_debug_set_pipeline_copy: copy
     engines pinned per direction -- the default --, HIP streams, HIP streams
     with a copy kernel for the outputs) gives the resident bits, over chunks
-    whose slots are reused (7 chunks on 3 slots, the last one partial).  The
+    whose slots are reused (8 chunks on 1-3 slots, the last one partial).  The
     default path runs on two different engines, whose overlap it measured at
-    creation."""
+    creation.  With one or two slots the H2D of plude (INOUT) into a reused
+    slot must wait for the D2H that reads the previous chunk's plude back out
+    of it: with one slot that D2H is the previous chunk's own."""
     ref = run_gpu(ds, 1000, 64, variant=ca.VARIANT_KCACHE)
     assert lib.cloudsc_debug_set_pipeline_copy(3) == ca.EINVAL
     try:
         for mode in (1, 0, 2):
             ca.check(lib.cloudsc_debug_set_pipeline_copy(mode))
-            hp = ca.HostPipeline(ds, 1000, 64, chunk_blocks=2, nstreams=3)
+            hp = ca.HostPipeline(ds, 1000, 64, chunk_blocks=2, nstreams=nstreams)
             try:
                 m, e_in, e_out = hp.copy_path()
                 if mode == 1:
