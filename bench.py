@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="host threads of the CPU baseline (default: OMP_NUM_THREADS, else all host cores)")
     p.add_argument("--no-hbm-peak", action="store_true", help="skip the in-run STREAM-copy measurement")
+    p.add_argument("--energy-seconds", type=float, default=2.0,
+                   help="after the timed region, run the kernel back to back this long while sampling the board's "
+                        "power (hwmon) for energy_uj_per_column; 0 skips it")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     a = p.parse_args()
@@ -219,11 +222,38 @@ def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
                     "cloudsc_driver.cu:344,456), host-buffer path over PCIe; NOT the headline value"}
 
 
+def energy_window(g, variant, cp, pw_file, seconds, ncols, np):
+    """Board power while the kernel runs back to back for `seconds` (after the
+    timed region, untimed): mean W over the window and the energy per column =
+    mean W x mean kernel time / columns.  The sensor averages over ~1-10 ms,
+    longer than one 1.6 ms launch, so the window is long; the timed region's
+    own mean W is reported beside it."""
+    if not pw_file:
+        return {"board_w": None, "energy_uj_per_column": None, "source": "no hwmon power file for this device"}
+    s = cp.PowerSampler(pw_file)
+    s.start()
+    t0, ms = time.perf_counter(), []
+    while time.perf_counter() - t0 < seconds:
+        ms.extend(g.run(variant, 50).tolist())
+    g.sync()
+    s.stop()
+    w = s.mean_w()
+    k = float(np.mean(ms))
+    return {"board_w": round(w, 1) if w else None,
+            "energy_uj_per_column": round(w * k * 1e-3 / ncols * 1e6, 3) if w else None,
+            "kernel_ms": round(k, 4), "launches": len(ms), "samples": len(s.samples),
+            "seconds": round(time.perf_counter() - t0, 2), "source": pw_file,
+            "method": "hwmon board power sampled every 10 ms while the kernel ran back to back after the timed "
+                      "region; energy per column = mean W x mean kernel time / columns (the reference reads "
+                      "energy beside its timings: EC_PMON, src/common/module/ec_pmon_mod.F90)"}
+
+
 def main():
     args = parse()
     import numpy as np
     import cloudsc_amd as ca
     import cloudsc_dist as cd
+    import cloudsc_power as cp
 
     topo = cd.topology_from_env()
     ctl = cd.Control(topo)               # gloo: barrier + max-over-ranks only
@@ -241,6 +271,10 @@ def main():
     # a 2-rank rehearsal on a 1-GPU box)
     device = topo.local_rank % ca.device_count()
     g = ca.GpuState(ds, ncols, args.nproma, prec, device=device, col_offset=col_offset)
+    # one launch timed alone, as the reference GPU driver times its single launch
+    # (cloudsc_driver.cu:389-422), right after creation (whose placement search
+    # has already run the kernel; the clock is not yet settled)
+    first_step_ms = float(g.run(variant, 1)[0])
     # The achievable-HBM (STREAM copy) measurement runs first: ~0.1 s of heavy
     # GPU work, after which the shader clock has left its idle level.  The
     # kernel's time follows the clock (profiles/r02/clock_probe_kseg_fp64.json:
@@ -254,15 +288,24 @@ def main():
     g.sync()
     if kind == ca.VARIANT_KSEG:
         g.kseg_clock(reset=True)                # the clock counters cover the timed launches only
+    pw_file = cp.power_file(device)
+    sampler = cp.PowerSampler(pw_file)
     ctl.barrier()
+    sampler.start()
     t0 = time.perf_counter()
     kernel_ms = g.run(variant, args.steps)      # one launch per step; its dispatch records its events
     g.sync()
     t1 = time.perf_counter()
+    sampler.stop()
     ctl.barrier()
     wall = ctl.max(t1 - t0)
     k_avg_ms = ctl.max(float(np.mean(kernel_ms)))
     sclk = g.kseg_clock() if kind == ca.VARIANT_KSEG else None
+    energy = energy_window(g, variant, cp, pw_file, args.energy_seconds, ncols, np) if args.energy_seconds > 0 \
+        else None
+    if energy is not None:
+        energy["timed_region_board_w"] = round(sampler.mean_w(), 1) if sampler.mean_w() else None
+        energy["timed_region_samples"] = len(sampler.samples)
     # every rank's own record, gathered to rank 0 (the reference's per-rank
     # timing table, src/common/module/timer_mod.F90:160-167)
     mine = {"rank": rank, "device": device, "local_rank": topo.local_rank, "ngptot": ncols,
@@ -271,7 +314,10 @@ def main():
             "kernel_ms_median": round(float(np.median(kernel_ms)), 4),
             "stream_gbs": round(peak_meas, 1) if peak_meas else None,
             "sclk_ghz": round(sclk, 4) if sclk else None, "prewarm_steps": prewarm,
-            "placement": g.placement()}
+            "first_step_ms": round(first_step_ms, 4),
+            "board_w": energy.get("board_w") if energy else None,
+            "energy_uj_per_column": energy.get("energy_uj_per_column") if energy else None,
+            "placement": g.placement_report()}
     per_rank = ctl.gather_records(mine)
 
     # validation of the last step against reference.h5 (device-side statistics, combined over ranks)
@@ -316,6 +362,9 @@ def main():
             "ngptot_per_gpu": args.ngptot, "ngptot_total": total_cols, "klev": ds.klev,
             "nproma": args.nproma, "variant": args.variant, "parallelism": "columns sharded, %d GPU(s)" % world},
         "prewarm_steps": prewarm,
+        "first_step_ms": round(first_step_ms, 4),
+        "first_step_method": "one launch timed alone right after state creation, as cloudsc_driver.cu:389-422 times "
+                             "its single launch (the placement search has run the kernel, the clock has not settled)",
         "kernel_ms": round(k_avg_ms, 4),
         "kernel_ms_min": round(float(np.min(kernel_ms)), 4),
         "kernel_ms_median": round(float(np.median(kernel_ms)), 4),
@@ -327,12 +376,14 @@ def main():
         "sclk_method": "effective shader clock of the timed launches: each workgroup's s_memtime cycles over its "
                        "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",
         "box": box_info() if rank == 0 else None,
-        "placement": dict(per_rank[0]["placement"], method=(
-            "output placement search at state creation (cloudsc_state_placement): the KSEG kernel on the state's "
-            "own inputs timed (best of 2) over candidate placements -- whole fresh output sets, one output field at "
-            "a time, then whole fresh input sets (the output and input sets after the first shuffled, with spacers) -- a candidate kept when it is > 1 % faster; probe ms of the "
-            "first and the kept "
-            "placement; rank 0")),
+        "placement": dict(per_rank[0]["placement"], how=(
+            "output placement search at state creation (cloudsc_state_placement_report): the KSEG kernel on the "
+            "state's own inputs timed (best of 2 after 1) over candidate placements -- 8 whole fresh output sets, "
+            "one output field at a time, then 4 whole fresh input sets (the sets after the first shuffled, with "
+            "spacers) -- a candidate kept when it is > 1 % faster; probe ms of the first and the kept placement, "
+            "its wall time, probe launches and the most candidate bytes held at once; rank 0; outside the timed "
+            "region")),
+        "energy": energy,
         "per_rank": per_rank,
         "validation_worst_rel_l1": worst,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -126,6 +126,23 @@ class Fields(C.Structure):
         "pfsqltur pfsqitur pfplsl pfplsn pfhpsl pfhpsn").split()]
 
 
+class Placement(C.Structure):
+    """cloudsc_placement_t: what a placement search cost and found."""
+    _fields_ = [("probe_first_ms", C.c_float), ("probe_final_ms", C.c_float), ("tries", C.c_int),
+                ("moves", C.c_int), ("launches", C.c_int), ("method", C.c_int), ("search_ms", C.c_double),
+                ("peak_transient_bytes", C.c_longlong)]
+
+    def to_dict(self) -> dict:
+        return {"probe_first_ms": round(self.probe_first_ms, 4), "probe_final_ms": round(self.probe_final_ms, 4),
+                "tries": self.tries, "moves": self.moves, "launches": self.launches,
+                "method": {0: "none", 1: "kernel", 2: "write-probe"}.get(self.method, self.method),
+                "search_ms": round(self.search_ms, 1), "peak_transient_bytes": self.peak_transient_bytes}
+
+
+PLACE_NONE = 1
+ALLOC_AEROSOLS = 2
+
+
 class Template(C.Structure):
     _fields_ = [("klon", C.c_int), ("klev", C.c_int)] + [(n, C.c_void_p) for n in (
         "pt pq tendency_tmp_t tendency_tmp_q tendency_tmp_a tendency_tmp_cld "
@@ -405,6 +422,13 @@ def gpu_lib(path: Optional[str] = None):
         lib.cloudsc_debug_host_pipeline_engine_check.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                                                  C.POINTER(C.c_int)]
         lib.cloudsc_host_pipeline_copy_bound.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    if hasattr(lib, "cloudsc_debug_memory_probe"):
+        lib.cloudsc_debug_memory_probe.argtypes = [C.c_int] * 5 + [C.POINTER(Fields), C.c_int, C.c_int,
+                                                                  C.POINTER(C.c_float)]
+    if hasattr(lib, "cloudsc_fields_alloc"):
+        lib.cloudsc_fields_alloc.argtypes = [C.c_int] * 6 + [C.POINTER(Fields), C.POINTER(Placement)]
+        lib.cloudsc_fields_free.argtypes = [C.c_int, C.POINTER(Fields)]
+        lib.cloudsc_state_placement_report.argtypes = [C.c_void_p, C.POINTER(Placement)]
     lib.cloudsc_gpu_init.argtypes = [C.c_int, C.POINTER(Params)]
     lib.cloudsc_gpu_run.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.POINTER(Fields), C.c_void_p]
@@ -591,6 +615,12 @@ class GpuState:
         return {"probe_first_ms": round(a.value, 4), "probe_final_ms": round(b.value, 4),
                 "tries": t.value, "moves": m.value}
 
+    def placement_report(self) -> dict:
+        """The placement search with its cost (cloudsc_state_placement_report)."""
+        r = Placement()
+        check(self.lib.cloudsc_state_placement_report(self.h, C.byref(r)))
+        return r.to_dict()
+
     def reset(self) -> None:
         check(self.lib.cloudsc_state_reset(self.h))
 
@@ -717,6 +747,82 @@ class HostPipeline:
         if getattr(self, "h", None):
             self.lib.cloudsc_host_pipeline_destroy(self.h)
             self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _hip():
+    h = C.CDLL("libamdhip64.so")
+    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    h.hipDeviceSynchronize.argtypes = []
+    h.hipSetDevice.argtypes = [C.c_int]
+    return h
+
+
+class DeviceFields:
+    """Caller-owned device fields (cloudsc_fields_alloc / cloudsc_fields_free):
+    the reference CUDA driver's shape -- allocate (cloudsc_driver.cu:276-328),
+    copy the inputs in, launch cloudsc_gpu_run (:391-416), copy the outputs
+    back (:425-447) -- with the output buffers placed by the library's
+    write-pattern search unless place=False."""
+
+    def __init__(self, ngptot: int, nproma: int, klev: int, precision: int = FP64, device: int = 0,
+                 place: bool = True, aerosols: bool = False):
+        self.lib = gpu_lib()
+        self.ngptot, self.nproma, self.klev, self.precision, self.device = ngptot, nproma, klev, precision, device
+        self.f = Fields()
+        self.report = Placement()
+        flags = (0 if place else PLACE_NONE) | (ALLOC_AEROSOLS if aerosols else 0)
+        check(self.lib.cloudsc_fields_alloc(device, precision, ngptot, nproma, klev, flags, C.byref(self.f),
+                                            C.byref(self.report)))
+        self.hip = _hip()
+
+    def nbytes(self, name: str) -> int:
+        es = 4 if name == "ktype" or self.precision == FP32 else 8
+        return nblocks_of(self.ngptot, self.nproma) * int(np.prod(field_shape(ALL_FIELDS[name], self.klev,
+                                                                             self.nproma))) * es
+
+    def copy_from(self, src: "Fields", names) -> None:
+        """Device-to-device copy of the named fields from another field set of
+        the same configuration (e.g. a state's, cloudsc_state_fields)."""
+        self.hip.hipSetDevice(self.device)
+        for n in names:
+            rc = self.hip.hipMemcpy(getattr(self.f, n), getattr(src, n), self.nbytes(n), 3)
+            if rc != 0:
+                raise CloudscError("hipMemcpy %s failed (%d)" % (n, rc))
+
+    def upload(self, arrays: Dict[str, np.ndarray]) -> None:
+        """Host block-layout arrays (make_host_state(...).arrays) into the device buffers."""
+        self.hip.hipSetDevice(self.device)
+        for n, a in arrays.items():
+            if getattr(self.f, n, None) is None:
+                continue
+            a = np.ascontiguousarray(a)
+            assert a.nbytes == self.nbytes(n), (n, a.nbytes, self.nbytes(n))
+            rc = self.hip.hipMemcpy(getattr(self.f, n), a.ctypes.data, a.nbytes, 1)
+            if rc != 0:
+                raise CloudscError("hipMemcpy %s failed (%d)" % (n, rc))
+
+    def download(self, name: str) -> np.ndarray:
+        """One field in block layout as float64."""
+        self.hip.hipSetDevice(self.device)
+        self.hip.hipDeviceSynchronize()
+        dt = np.int32 if name == "ktype" else (np.float64 if self.precision == FP64 else np.float32)
+        nb = nblocks_of(self.ngptot, self.nproma)
+        out = np.empty((nb,) + field_shape(ALL_FIELDS[name], self.klev, self.nproma), dtype=dt)
+        rc = self.hip.hipMemcpy(out.ctypes.data, getattr(self.f, name), out.nbytes, 2)
+        if rc != 0:
+            raise CloudscError("hipMemcpy %s failed (%d)" % (name, rc))
+        return out.astype(np.float64)
+
+    def close(self) -> None:
+        if getattr(self, "f", None) is not None:
+            self.lib.cloudsc_fields_free(self.device, C.byref(self.f))
+            self.f = None
 
     def __del__(self):
         try:

@@ -4,11 +4,49 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+#include <functional>
+
 #include "cloudsc_amd.h"
 
 namespace cloudsc_impl {
 
 constexpr int kMaxDevices = 64;
+
+// The fields of cloudsc_fields_t: shape kind, direction, element type, in
+// member order (include/cloudsc_amd.h).
+enum FieldKind { FK_LEVEL, FK_HALF, FK_SPECIES, FK_SURFACE };
+enum FieldDir { FD_IN, FD_INOUT, FD_OUT, FD_AEROSOL };
+struct FieldDesc { int kind, dir, is_int; };
+// cloudsc_fields_t member order (include/cloudsc_amd.h)
+inline constexpr FieldDesc kFieldTable[] = {
+    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_IN, 0},   {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_HALF, FD_IN, 0},    {FK_SURFACE, FD_IN, 0}, {FK_SURFACE, FD_IN, 1}, {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
+    {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},
+    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
+    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
+    {FK_LEVEL, FD_INOUT, 0},
+    {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_SPECIES, FD_OUT, 0},
+    {FK_LEVEL, FD_OUT, 0},  {FK_SURFACE, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
+    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0}};
+inline constexpr int kNumFields = (int)(sizeof(kFieldTable) / sizeof(kFieldTable[0]));
+static_assert(sizeof(cloudsc_fields_t) == kNumFields * sizeof(void*), "field table out of sync with the header");
+
+inline size_t per_block_elems(int kind, int nproma, int klev) {
+  switch (kind) {
+    case FK_LEVEL: return (size_t)klev * nproma;
+    case FK_HALF: return (size_t)(klev + 1) * nproma;
+    case FK_SPECIES: return (size_t)CLOUDSC_NCLV * klev * nproma;
+    default: return (size_t)nproma;
+  }
+}
+
 
 // One parameter set on one device: the host-folded fp64 and fp32 DevParams
 // blocks in device memory (read by the kernels through a KArgs pointer), plus
@@ -66,6 +104,32 @@ int kseg_check(int device, void* stream, void* scratch);
 // real-time ticks of the workgroups, times the real-time rate) and the summed
 // workgroup-seconds behind it; reset zeroes the sums
 int kseg_clock(int device, void* stream, void* scratch, bool reset, double* ghz, double* seconds);
+
+// the memory-pattern probe of cloudsc_place.hip over f on `stream`: best of
+// `reps` timed launches after one untimed, ms; mode 0 outputs written only, 1
+// inputs read too (every non-NULL output of f is overwritten)
+int memory_probe(int device, hipStream_t stream, int precision, int ngptot, int nproma, int klev,
+                 const cloudsc_fields_t* f, int mode, int reps, hipEvent_t e0, hipEvent_t e1, float* best_ms);
+
+// What a placement search cost and found (cloudsc_place.hip)
+struct PlaceCost {
+  float first_ms = 0.f, final_ms = 0.f;   // probe time of the first / the kept placement
+  int tries = 0, moves = 0;               // candidate buffers allocated / kept
+  int launches = 0;                       // probe launches (untimed ones included)
+  double search_ms = 0.0;                 // wall time of the search
+  long long peak_bytes = 0;               // most candidate and spacer bytes held at once
+};
+// the output placement search (see cloudsc_place.hip): moves f's output
+// members (members/bytes: positions in cloudsc_fields_t and sizes) to the
+// fastest candidate buffers under `probe` (ms, < 0 on an error); never frees
+// the caller's original buffers
+int search_outputs(cloudsc_fields_t& f, const int* members, const size_t* bytes, int n, int sets, int passes,
+                   uint32_t seed, const std::function<float(const cloudsc_fields_t&)>& probe, PlaceCost& cost);
+
+// whether a placement search whose candidates peak at about `transient` bytes
+// fits the device's free memory with room to spare (on a device
+// shared by several ranks the search must not starve their allocations)
+bool search_fits(size_t transient);
 
 // copy ceiling on the pipelines' engine pair (cloudsc_pipeline.hip)
 int pcie_engine_gbps(int device, size_t nb, int reps, double* h2d, double* d2h, double* both);

@@ -47,41 +47,7 @@ using namespace cloudsc_impl;
 // chunked SCC pipeline after other pipelines had come and gone).  So the page
 // ranges of all fields are merged first and every merged range is registered
 // once: each array lies wholly inside exactly one registration.
-namespace {
-
-enum FieldKind { FK_LEVEL, FK_HALF, FK_SPECIES, FK_SURFACE };
-enum FieldDir { FD_IN, FD_INOUT, FD_OUT, FD_AEROSOL };
-struct FieldDesc { int kind, dir, is_int; };
-// cloudsc_fields_t member order (include/cloudsc_amd.h)
-constexpr FieldDesc kFieldTable[] = {
-    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_IN, 0},   {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_HALF, FD_IN, 0},    {FK_SURFACE, FD_IN, 0}, {FK_SURFACE, FD_IN, 1}, {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},   {FK_LEVEL, FD_IN, 0},
-    {FK_SPECIES, FD_IN, 0}, {FK_LEVEL, FD_IN, 0},
-    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
-    {FK_LEVEL, FD_AEROSOL, 0}, {FK_LEVEL, FD_AEROSOL, 0},
-    {FK_LEVEL, FD_INOUT, 0},
-    {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_LEVEL, FD_OUT, 0},  {FK_SPECIES, FD_OUT, 0},
-    {FK_LEVEL, FD_OUT, 0},  {FK_SURFACE, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0},
-    {FK_HALF, FD_OUT, 0},   {FK_HALF, FD_OUT, 0}};
-constexpr int kNumFields = (int)(sizeof(kFieldTable) / sizeof(kFieldTable[0]));
-static_assert(sizeof(cloudsc_fields_t) == kNumFields * sizeof(void*), "field table out of sync with the header");
-
-size_t per_block_elems(int kind, int nproma, int klev) {
-  switch (kind) {
-    case FK_LEVEL: return (size_t)klev * nproma;
-    case FK_HALF: return (size_t)(klev + 1) * nproma;
-    case FK_SPECIES: return (size_t)CLOUDSC_NCLV * klev * nproma;
-    default: return (size_t)nproma;
-  }
-}
-
-}  // namespace
+// (The field table, kFieldTable, is in cloudsc_internal.h.)
 
 // D2H of one chunk by a copy kernel instead of the copy engine (diagnostic
 // mode 2 of cloudsc_debug_set_pipeline_copy): every output field's chunk range,

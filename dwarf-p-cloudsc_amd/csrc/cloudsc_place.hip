@@ -1,0 +1,447 @@
+// cloudsc_place.hip -- placement of the fields in HBM (round 5).
+//
+// The rate at which the CLOUDSC kernel writes its 21 output fields depends on
+// where they land in HBM: states of one configuration ran 1.63-1.94 ms (fp64
+// KSEG), and the slow states stall 5-10x longer on DRAM write credits
+// (DESIGN.md §3.12).  This file holds the measuring instrument that needs no
+// field contents: a memory-pattern probe that streams a field set the way the
+// KSEG kernel does -- one wave per 64-column sub-block, level by level, each
+// input plane read and each output plane written once, non-temporal -- with no
+// physics.  Its time on a set of device pointers ranks placements without the
+// caller's inputs (tools/place_corr.py measures how well it ranks them against
+// the physics kernel).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "cloudsc_internal.h"
+
+using namespace cloudsc_impl;
+
+namespace {
+
+constexpr int kProbeInLevel = 17;   // level inputs, one plane each
+constexpr int kProbeOutLevel = 5;   // level outputs, one plane each (plude, tendency_loc_t/q/a, pcovptot)
+constexpr int kProbeOutHalf = 14;   // flux outputs, written at level k+1
+constexpr int kPlaceSetsFields = 8; // whole output sets tried by cloudsc_fields_alloc
+
+struct ProbeArgs {
+  const void* in_level[kProbeInLevel];
+  const void* in_species[2];          // tendency_tmp_cld, pclv: species 0..3 read
+  const void* paph;                   // half-level input
+  void* out_level[kProbeOutLevel];
+  void* out_species;                  // tendency_loc_cld: species 0..4 written
+  void* out_half[kProbeOutHalf];
+  void* out_surf;                     // prainfrac_toprfz
+  int ngptot, nproma, klev, nsub, nitems;
+};
+
+template <typename real>
+__device__ __forceinline__ real ldnt(const void* p, size_t i) {
+  return __builtin_nontemporal_load((const real*)p + i);
+}
+template <typename real>
+__device__ __forceinline__ void stnt(void* p, size_t i, real v) {
+  __builtin_nontemporal_store(v, (real*)p + i);
+}
+
+// one wave per item (64-column sub-block of an NPROMA block); a grid of at most
+// 2048 one-wave workgroups (two per SIMD, like the KSEG kernel) strides the
+// items.  READ: the level-(k+1) input planes are loaded while level k's outputs
+// are stored (one level of lookahead, like the kernel's prefetch), and their
+// sum goes to the surface output at the end; the stored values do not depend
+// on the loads, so stores never wait for them.
+template <typename real, bool READ>
+__global__ void __launch_bounds__(64) place_probe_kernel(const ProbeArgs a) {
+  constexpr int NL = READ ? kProbeInLevel + 9 : 1;   // level planes + 8 species planes + paph
+  const int lane = threadIdx.x;
+  for (int it = blockIdx.x; it < a.nitems; it += gridDim.x) {
+    const long long b = it / a.nsub;
+    const int sub = it - (int)(b * a.nsub);
+    const int jl = sub * 64 + lane;
+    const long long col = b * a.nproma + jl;
+    if (jl >= a.nproma || col >= a.ngptot) continue;
+    const size_t np = (size_t)a.nproma, kl = (size_t)a.klev;
+    const size_t lvl0 = (size_t)b * kl * np + jl, half0 = (size_t)b * (kl + 1) * np + jl;
+    const size_t spc0 = (size_t)b * 5 * kl * np + jl;
+    real acc = (real)0, nxt[NL];
+    auto load = [&](int k) {
+      if constexpr (READ) {
+        const size_t il = lvl0 + (size_t)k * np;
+#pragma unroll
+        for (int q = 0; q < kProbeInLevel; q++) nxt[q] = a.in_level[q] ? ldnt<real>(a.in_level[q], il) : (real)0;
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+          for (int s = 0; s < 4; s++)
+            nxt[kProbeInLevel + 4 * q + s] =
+                a.in_species[q] ? ldnt<real>(a.in_species[q], spc0 + ((size_t)s * kl + k) * np) : (real)0;
+        nxt[NL - 1] = a.paph ? ldnt<real>(a.paph, half0 + (size_t)(k + 1) * np) : (real)0;
+      }
+    };
+    load(0);
+    const real v0 = (real)b;
+#pragma unroll
+    for (int q = 0; q < kProbeOutHalf; q++)
+      if (a.out_half[q]) stnt<real>(a.out_half[q], half0, v0);
+    for (int k = 0; k < a.klev; k++) {
+      real cur[NL];
+#pragma unroll
+      for (int q = 0; q < NL; q++) cur[q] = nxt[q];
+      if (k + 1 < a.klev) load(k + 1);
+      const size_t il = lvl0 + (size_t)k * np;
+      const real v = v0 + (real)k;
+#pragma unroll
+      for (int q = 0; q < kProbeOutLevel; q++)
+        if (a.out_level[q]) stnt<real>(a.out_level[q], il, v);
+      if (a.out_species)
+#pragma unroll
+        for (int s = 0; s < 5; s++) stnt<real>(a.out_species, spc0 + ((size_t)s * kl + k) * np, v);
+#pragma unroll
+      for (int q = 0; q < kProbeOutHalf; q++)
+        if (a.out_half[q]) stnt<real>(a.out_half[q], half0 + (size_t)(k + 1) * np, v);
+      if constexpr (READ) {
+#pragma unroll
+        for (int q = 0; q < NL; q++) acc += cur[q];
+      }
+    }
+    if (a.out_surf) stnt<real>(a.out_surf, (size_t)b * np + jl, acc);
+  }
+}
+
+ProbeArgs probe_args(const cloudsc_fields_t* f, int ngptot, int nproma, int klev, bool read) {
+  ProbeArgs a;
+  std::memset(&a, 0, sizeof(a));
+  if (read) {
+    const void* lv[kProbeInLevel] = {f->pt, f->pq, f->tendency_tmp_t, f->tendency_tmp_q, f->tendency_tmp_a,
+                                     f->pvfl, f->pvfi, f->phrsw, f->phrlw, f->pvervel, f->pap, f->plu,
+                                     f->psnde, f->pmfu, f->pmfd, f->pa, f->psupsat};
+    for (int q = 0; q < kProbeInLevel; q++) a.in_level[q] = lv[q];
+    a.in_species[0] = f->tendency_tmp_cld;
+    a.in_species[1] = f->pclv;
+    a.paph = f->paph;
+  }
+  void* ol[kProbeOutLevel] = {f->plude, f->tendency_loc_t, f->tendency_loc_q, f->tendency_loc_a, f->pcovptot};
+  for (int q = 0; q < kProbeOutLevel; q++) a.out_level[q] = ol[q];
+  a.out_species = f->tendency_loc_cld;
+  void* oh[kProbeOutHalf] = {f->pfsqlf, f->pfsqif, f->pfcqnng, f->pfcqlng, f->pfsqrf, f->pfsqsf, f->pfcqrng,
+                             f->pfcqsng, f->pfsqltur, f->pfsqitur, f->pfplsl, f->pfplsn, f->pfhpsl, f->pfhpsn};
+  for (int q = 0; q < kProbeOutHalf; q++) a.out_half[q] = oh[q];
+  a.out_surf = f->prainfrac_toprfz;
+  a.ngptot = ngptot;
+  a.nproma = nproma;
+  a.klev = klev;
+  a.nsub = (nproma + 63) / 64;
+  const long long nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
+  a.nitems = (int)(nblocks * a.nsub);
+  return a;
+}
+
+}  // namespace
+
+namespace cloudsc_impl {
+
+// time of the memory-pattern probe over f on `stream`, best of `reps` after
+// one untimed launch, in ms; mode 0 writes the outputs only, 1 also reads the
+// inputs.  Every non-NULL output of f is overwritten.
+int memory_probe(int device, hipStream_t stream, int precision, int ngptot, int nproma, int klev,
+                 const cloudsc_fields_t* f, int mode, int reps, hipEvent_t e0, hipEvent_t e1, float* best_ms) {
+  const ProbeArgs a = probe_args(f, ngptot, nproma, klev, mode == 1);
+  const dim3 grid((unsigned)std::min(a.nitems, 2048));
+  float best = -1.f;
+  for (int r = 0; r <= reps; r++) {
+    HIPCHK(hipEventRecord(e0, stream));
+    if (precision == CLOUDSC_FP64) {
+      if (mode == 1) hipLaunchKernelGGL((place_probe_kernel<double, true>), grid, dim3(64), 0, stream, a);
+      else hipLaunchKernelGGL((place_probe_kernel<double, false>), grid, dim3(64), 0, stream, a);
+    } else {
+      if (mode == 1) hipLaunchKernelGGL((place_probe_kernel<float, true>), grid, dim3(64), 0, stream, a);
+      else hipLaunchKernelGGL((place_probe_kernel<float, false>), grid, dim3(64), 0, stream, a);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e1, stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, e0, e1));
+    if (r > 0 && (best < 0.f || t < best)) best = t;
+  }
+  (void)device;
+  *best_ms = best;
+  return CLOUDSC_OK;
+}
+
+bool search_fits(size_t transient) {
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) { (void)hipGetLastError(); return false; }
+  return free_b >= transient + transient / 2 + ((size_t)1 << 30);
+}
+
+// ---------------------------------------------------------------------------
+// Output placement search, shared by the state (probe = the KSEG kernel on the
+// state's inputs) and cloudsc_fields_alloc (probe = the write pattern above,
+// which needs no contents).  Candidates: `sets` whole fresh output sets (the
+// first in field order, the others shuffled with a spacer of 2-32 MiB before
+// each field, so the fields' relative physical placement changes, not just the
+// set's base), then `passes` rounds of one field at a time; a candidate is kept
+// when the probe is > 1 % faster.  The caller's original buffers are never
+// freed here: on return f holds the chosen pointers and the caller adopts the
+// new ones (and frees the originals they replaced) or reverts.  Every other
+// candidate is freed before return; rejected buffers are held until then, so
+// no retry gets the same pages back.  An allocation failure ends the phase
+// with the best placement so far.
+int search_outputs(cloudsc_fields_t& f, const int* members, const size_t* bytes, int n, int sets, int passes,
+                   uint32_t seed, const std::function<float(const cloudsc_fields_t&)>& probe, PlaceCost& cost) {
+  const auto t0 = std::chrono::steady_clock::now();
+  cloudsc_fields_t orig = f;
+  void** bf = (void**)&f;
+  void** of = (void**)&orig;
+  std::vector<std::pair<void*, size_t>> held;   // rejected or replaced candidates, freed at the end
+  size_t live = 0;                              // candidate bytes held beyond the caller's set
+  auto note = [&]() { cost.peak_bytes = std::max(cost.peak_bytes, (long long)live); };
+  bool room = true;
+  auto fresh = [&](size_t nb) -> void* {
+    void* q = nullptr;
+    if (!room || hipMalloc(&q, nb) != hipSuccess) { (void)hipGetLastError(); room = false; return nullptr; }
+    live += nb;
+    note();
+    return q;
+  };
+  auto drop = [&](void* p, size_t nb) { (void)hipFree(p); live -= nb; };
+  auto is_orig = [&](int q) { return bf[members[q]] == of[members[q]]; };
+  float best = probe(f);
+  if (best < 0.f) return CLOUDSC_EHIP;
+  cost.first_ms = best;
+  uint32_t rng = seed;
+  auto next = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
+  int rc = CLOUDSC_OK;
+  std::vector<std::pair<void*, size_t>> spacers;
+  for (int k = 0; k < sets && room && rc == CLOUDSC_OK; k++) {
+    cloudsc_fields_t cand = f;
+    void** cf = (void**)&cand;
+    std::vector<int> order(n);
+    for (int q = 0; q < n; q++) order[q] = q;
+    if (k > 0)
+      for (int q = n - 1; q > 0; q--) std::swap(order[q], order[next() % (q + 1)]);
+    int got = 0;
+    for (int i = 0; i < n; i++) {
+      const int q = order[i];
+      if (k > 0) {
+        const size_t sb = ((size_t)1 + next() % 16) << 21;
+        void* sp = fresh(sb);
+        if (!sp) break;
+        spacers.push_back({sp, sb});
+      }
+      void* p = fresh(bytes[q]);
+      if (!p) break;
+      cf[members[q]] = p;
+      got++;
+    }
+    if (got < n) {
+      for (int i = 0; i < got; i++) drop(cf[members[order[i]]], bytes[order[i]]);
+      break;
+    }
+    const float t = probe(cand);
+    cost.tries += n;
+    if (t < 0.f) { rc = CLOUDSC_EHIP; for (int q = 0; q < n; q++) drop(cf[members[q]], bytes[q]); break; }
+    if (t < best * 0.99f) {
+      // the set it replaces: the caller's originals stay theirs, earlier candidates go
+      for (int q = 0; q < n; q++)
+        if (!is_orig(q)) drop(bf[members[q]], bytes[q]);
+      f = cand; best = t; cost.moves += n;
+    } else {
+      for (int q = 0; q < n; q++) drop(cf[members[q]], bytes[q]);
+    }
+  }
+  for (auto& sp : spacers) drop(sp.first, sp.second);
+  room = true;
+  for (int pass = 0; pass < passes && room && rc == CLOUDSC_OK; pass++) {
+    int moved = 0;
+    for (int q = 0; q < n && rc == CLOUDSC_OK; q++) {
+      void* p = fresh(bytes[q]);
+      if (!p) break;
+      void* old = bf[members[q]];
+      bf[members[q]] = p;
+      const float t = probe(f);
+      cost.tries++;
+      if (t < 0.f) { rc = CLOUDSC_EHIP; bf[members[q]] = old; held.push_back({p, bytes[q]}); break; }
+      if (t < best * 0.99f) {
+        best = t; moved++; cost.moves++;
+        if (old != of[members[q]]) held.push_back({old, bytes[q]});
+      } else {
+        bf[members[q]] = old;
+        held.push_back({p, bytes[q]});
+      }
+    }
+    if (!moved) break;
+  }
+  for (auto& h : held) drop(h.first, h.second);
+  cost.final_ms = best;
+  cost.search_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+}  // namespace cloudsc_impl
+
+extern "C" int cloudsc_debug_memory_probe(int device, int precision, int ngptot, int nproma, int klev,
+                                          const cloudsc_fields_t* f, int mode, int reps, float* ms) {
+  if (!f || !ms || reps <= 0 || (mode != 0 && mode != 1)) return CLOUDSC_EINVAL;
+  int rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KSEG, ngptot, nproma, klev);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) rc = CLOUDSC_EHIP;
+  if (!rc) rc = memory_probe(device, st, precision, ngptot, nproma, klev, f, mode, reps, e0, e1, ms);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI: caller-owned field sets with a placement search (round 5).  The
+// reference GPU driver allocates its device arrays itself
+// (src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:276-328) and launches on them
+// (:391-416); cloudsc_gpu_run is that launch.  cloudsc_fields_alloc is the
+// allocation: one device buffer per field, and -- unless the caller runs a
+// single step -- the output buffers placed by the write-pattern probe, which
+// needs no field contents, so the caller fills the inputs afterwards.
+// ---------------------------------------------------------------------------
+namespace {
+
+std::mutex g_fields_mu;
+std::unordered_map<void*, int> g_fields_allocs;   // buffer -> device, for cloudsc_fields_free
+
+void fields_register(void* p, int device) {
+  std::lock_guard<std::mutex> lk(g_fields_mu);
+  g_fields_allocs[p] = device;
+}
+bool fields_unregister(void* p, int device) {
+  std::lock_guard<std::mutex> lk(g_fields_mu);
+  auto it = g_fields_allocs.find(p);
+  if (it == g_fields_allocs.end() || it->second != device) return false;
+  g_fields_allocs.erase(it);
+  return true;
+}
+
+size_t member_bytes(int m, int precision, int ngptot, int nproma, int klev) {
+  const FieldDesc& d = kFieldTable[m];
+  const size_t nb = (size_t)(ngptot / nproma + (ngptot % nproma ? 1 : 0));
+  const size_t es = d.is_int ? sizeof(int) : precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
+  return nb * per_block_elems(d.kind, nproma, klev) * es;
+}
+
+}  // namespace
+
+extern "C" int cloudsc_fields_free(int device, cloudsc_fields_t* f);
+
+extern "C" int cloudsc_fields_alloc(int device, int precision, int ngptot, int nproma, int klev, int flags,
+                                    cloudsc_fields_t* out, cloudsc_placement_t* report) {
+  if (!out || (flags & ~(CLOUDSC_PLACE_NONE | CLOUDSC_ALLOC_AEROSOLS))) return CLOUDSC_EINVAL;
+  int rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KSEG, ngptot, nproma, klev);
+  if (rc) return rc;
+  std::memset(out, 0, sizeof(*out));
+  if (report) std::memset(report, 0, sizeof(*report));
+  HIPCHK(hipSetDevice(device));
+  void** df = (void**)out;
+  for (int m = 0; m < kNumFields; m++) {
+    if (kFieldTable[m].dir == FD_AEROSOL && !(flags & CLOUDSC_ALLOC_AEROSOLS)) continue;
+    void* p = nullptr;
+    const hipError_t e = hipMalloc(&p, member_bytes(m, precision, ngptot, nproma, klev));
+    if (e != hipSuccess) {
+      hip_fail(e, "hipMalloc");
+      cloudsc_fields_free(device, out);
+      return CLOUDSC_ENOMEM;
+    }
+    fields_register(p, device);
+    df[m] = p;
+  }
+  if (flags & CLOUDSC_PLACE_NONE) return CLOUDSC_OK;
+  // the search: output members and sizes, the write probe on a stream of its own
+  int members[kNumFields];
+  size_t bytes[kNumFields], set_bytes = 0;
+  int n = 0;
+  for (int m = 0; m < kNumFields; m++)
+    if (kFieldTable[m].dir == FD_OUT || kFieldTable[m].dir == FD_INOUT) {
+      members[n] = m;
+      bytes[n] = member_bytes(m, precision, ngptot, nproma, klev);
+      set_bytes += bytes[n++];
+    }
+  // two candidate sets and their spacers at most (search_outputs)
+  if (!search_fits(2 * set_bytes + ((size_t)n << 25))) return CLOUDSC_OK;   // no room: no search (method NONE)
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  PlaceCost cost;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+      hipEventCreate(&e1) != hipSuccess)
+    rc = hip_fail(hipGetLastError(), "fields_alloc stream/events");
+  auto probe = [&](const cloudsc_fields_t& f) -> float {
+    float ms = -1.f;
+    cost.launches += 3;
+    if (memory_probe(device, st, precision, ngptot, nproma, klev, &f, 0, 2, e0, e1, &ms) != CLOUDSC_OK) return -1.f;
+    return ms;
+  };
+  // the shader clock leaves its idle level over the first ~25 ms of work
+  // (DESIGN.md §3.8): warm it before the first placement is timed
+  for (int w = 0; w < 10 && !rc; w++)
+    if (probe(*out) < 0.f) rc = CLOUDSC_EHIP;
+  cloudsc_fields_t before = *out;
+  if (!rc) rc = search_outputs(*out, members, bytes, n, kPlaceSetsFields, 2, 0x9e3779b9u ^ (uint32_t)ngptot, probe,
+                               cost);
+  // adopt the chosen buffers, free the originals they replaced (or, on an
+  // error, keep the originals)
+  void** bf = (void**)&before;
+  for (int q = 0; q < n; q++) {
+    const int m = members[q];
+    if (df[m] == bf[m]) continue;
+    void* drop = rc ? df[m] : bf[m];
+    if (rc) df[m] = bf[m];
+    else fields_register(df[m], device);
+    if (!rc) fields_unregister(bf[m], device);
+    (void)hipFree(drop);
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) { (void)hipStreamSynchronize(st); (void)hipStreamDestroy(st); }
+  if (rc) {
+    cloudsc_fields_free(device, out);
+    return rc;
+  }
+  if (report) {
+    report->probe_first_ms = cost.first_ms;
+    report->probe_final_ms = cost.final_ms;
+    report->tries = cost.tries;
+    report->moves = cost.moves;
+    report->launches = cost.launches;
+    report->search_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    report->peak_transient_bytes = cost.peak_bytes;
+    report->method = CLOUDSC_PLACE_METHOD_WRITE_PROBE;
+  }
+  return CLOUDSC_OK;
+}
+
+extern "C" int cloudsc_fields_free(int device, cloudsc_fields_t* f) {
+  if (!f) return CLOUDSC_EINVAL;
+  int rc = CLOUDSC_OK;
+  if (hipSetDevice(device) != hipSuccess) return CLOUDSC_ENODEV;
+  void** df = (void**)f;
+  for (int m = 0; m < kNumFields; m++) {
+    if (!df[m]) continue;
+    if (fields_unregister(df[m], device)) {
+      (void)hipFree(df[m]);
+      df[m] = nullptr;
+    } else {
+      rc = CLOUDSC_EINVAL;   // not a buffer of cloudsc_fields_alloc on this device: left alone
+    }
+  }
+  return rc;
+}

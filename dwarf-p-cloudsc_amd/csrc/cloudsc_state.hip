@@ -2,8 +2,11 @@
 // (cloudsc_state_*): on-device expansion of the KLON-column template (g % klon
 // of the GLOBAL column index), timed runs on the state's stream, and on-device
 // validation statistics against the KLON-column reference.
+#include <algorithm>
 #include <atomic>
 #include <hip/hip_runtime.h>
+
+#include <chrono>
 
 #include <cstdio>
 #include <cstring>
@@ -115,6 +118,7 @@ struct cloudsc_gpu_state {
   size_t fbytes[sizeof(cloudsc_fields_t) / sizeof(void*)];   // bytes of each field, cloudsc_fields_t order
   float place_first_ms = 0.f, place_final_ms = 0.f;           // output write probe before / after the search
   int place_tries = 0, place_moves = 0;
+  cloudsc_impl::PlaceCost pcost;                              // the search's cost (both phases)
 };
 
 namespace {
@@ -194,9 +198,10 @@ int field_alloc(cloudsc_gpu_state* s, Arena& ar, void** p, size_t bytes) {
 // state times the physics kernel itself (KSEG, on the state's inputs) over
 // candidate placements of its outputs: whole fresh output sets first, then one
 // field at a time, keeping a candidate only if the kernel time drops by more
-// than 1 %.  Rejected allocations are held until the search ends, so no retry
-// gets the same pages back; an allocation failure ends the search with the
-// best placement so far.  Outputs are written before the search's launches
+// than 1 % (search_outputs, cloudsc_place.hip: a rejected set is freed at once
+// behind spacers that keep the next set off its pages, rejected single fields
+// are held until the search ends); an allocation failure ends the search with
+// the best placement so far.  Outputs are written before the search's launches
 // only by those launches and are reset afterwards: the results do not depend
 // on it (cloudsc_debug_set_placement_search turns it off).
 std::atomic<int> g_place_passes{2};   // cloudsc_debug_set_placement_search
@@ -228,131 +233,61 @@ void dfree(cloudsc_gpu_state* s, void* p) {
   (void)hipFree(p);
 }
 
-// members/bytes: the output fields (positions in cloudsc_fields_t); moves s->f's pointers
+// members/bytes: the output fields (positions in cloudsc_fields_t); moves
+// s->f's pointers.  The search itself is search_outputs (cloudsc_place.hip)
+// with the KSEG kernel on the state's own inputs as the probe.
 int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, int n) {
   const int passes = g_place_passes.load();
   if (passes <= 0) return CLOUDSC_OK;
-  cloudsc_fields_t best_f = s->f;
-  void** bf = (void**)&best_f;
+  PlaceCost& cost = s->pcost;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto probe = [&](const cloudsc_fields_t& f) {
+    cost.launches += 3;
+    return probe_kernel(s, f);
+  };
   // the shader clock leaves its idle level over the first ~10-15 launches
   // (bench.py prewarm): warm it before the first time is taken
   for (int w = 0; w < 4; w++)
-    if (probe_kernel(s, best_f) < 0.f) return CLOUDSC_EHIP;
-  float best = probe_kernel(s, best_f);
-  if (best < 0.f) return CLOUDSC_EHIP;
-  s->place_first_ms = best;
-  std::vector<void*> held;          // every candidate buffer not (yet) chosen, freed at the end
-  bool room = true;
-  auto fresh = [&](size_t nb) -> void* {
-    void* q = nullptr;
-    if (!room || hipMalloc(&q, nb) != hipSuccess) { (void)hipGetLastError(); room = false; return nullptr; }
-    return q;
-  };
-  int rc = CLOUDSC_OK;
-  // whole fresh output sets: the first in field order, the others in a
-  // shuffled order with a spacer of 2-32 MiB before each field, so that the
-  // fields' relative physical placement changes, not just the set's base (with
-  // plain sets one searched state in six kept its slow time,
-  // profiles/r04/placement/placement_search_ab_fp64.jsonl).  A rejected set
-  // is freed at once (the spacers, held to the end of this phase, keep the next
-  // set off its pages), so the phase holds at most two output sets.
-  std::vector<void*> spacers;
-  uint32_t rng = 0x9e3779b9u ^ (uint32_t)(uintptr_t)s;
-  auto next = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
-  auto owned = [&](void* p) {
-    for (void* q : s->allocs)
-      if (q == p) return true;
-    return false;
-  };
-  auto release = [&](void* p) {     // the state's first allocation is held to the end (a timed-out search reverts)
-    if (owned(p)) held.push_back(p); else (void)hipFree(p);
-  };
-  for (int k = 0; k < kPlaceSets && room && rc == CLOUDSC_OK; k++) {
-    cloudsc_fields_t cand = best_f;
-    void** cf = (void**)&cand;
-    int order[64];
-    for (int q = 0; q < n; q++) order[q] = q;
-    if (k > 0)
-      for (int q = n - 1; q > 0; q--) std::swap(order[q], order[next() % (q + 1)]);
-    int got = 0;
-    for (int i = 0; i < n; i++) {
-      const int q = order[i];
-      if (k > 0) {
-        void* sp = fresh(((size_t)1 + next() % 16) << 21);
-        if (!sp) break;
-        spacers.push_back(sp);
-      }
-      void* p = fresh(bytes[q]);
-      if (!p) break;
-      cf[members[q]] = p;
-      got++;
-    }
-    if (got < n) {
-      for (int i = 0; i < got; i++) (void)hipFree(cf[members[order[i]]]);
-      break;
-    }
-    const float t = probe_kernel(s, cand);
-    s->place_tries += n;
-    if (t < 0.f) { rc = CLOUDSC_EHIP; for (int q = 0; q < n; q++) (void)hipFree(cf[members[q]]); break; }
-    if (t < best * 0.99f) {
-      for (int q = 0; q < n; q++) release(bf[members[q]]);
-      best_f = cand; best = t; s->place_moves += n;
-    } else {
-      for (int q = 0; q < n; q++) (void)hipFree(cf[members[q]]);
-    }
-  }
-  for (void* p : spacers) (void)hipFree(p);
-  room = true;
-  // one field at a time
-  for (int pass = 0; pass < passes && room && rc == CLOUDSC_OK; pass++) {
-    int moved = 0;
-    for (int q = 0; q < n && rc == CLOUDSC_OK; q++) {
-      void* p = fresh(bytes[q]);
-      if (!p) break;
-      void* old = bf[members[q]];
-      bf[members[q]] = p;
-      const float t = probe_kernel(s, best_f);
-      s->place_tries++;
-      if (t < 0.f) { rc = CLOUDSC_EHIP; bf[members[q]] = old; held.push_back(p); break; }
-      if (t < best * 0.99f) { best = t; moved++; s->place_moves++; held.push_back(old); }
-      else { bf[members[q]] = old; held.push_back(p); }
-    }
-    if (!moved) break;
-  }
+    if (probe(s->f) < 0.f) return CLOUDSC_EHIP;
+  cloudsc_fields_t f = s->f;
+  int rc = search_outputs(f, members, bytes, n, kPlaceSets, passes, 0x9e3779b9u ^ (uint32_t)(uintptr_t)s, probe,
+                          cost);
+  void** bf = (void**)&f;
   void** sf = (void**)&s->f;
   // probes whose segment hand-offs timed out (the diagnostic spin limit, or a
   // real fault of the schedule) timed nothing meaningful: keep the first
   // placement, clear the workspace's error and record the search as abandoned
   // (probe_final_ms < 0); a KSEG run of the state reports such a fault itself
+  bool revert = rc != CLOUDSC_OK;
   if (rc == CLOUDSC_OK) {
     const int hc = kseg_check(s->device, s->stream, s->kseg_ws);
     if (hc == CLOUDSC_EHANDOFF) {
-      for (int q = 0; q < n; q++) {
-        const int m = members[q];
-        if (bf[m] == sf[m]) continue;
-        for (auto& h : held)
-          if (h == sf[m]) { h = held.back(); held.pop_back(); break; }
-        held.push_back(bf[m]);
-        bf[m] = sf[m];
-      }
-      s->place_moves = 0;
-      best = -1.f;
+      revert = true;
+      cost.moves = 0;
+      cost.final_ms = -1.f;
     } else {
       rc = hc;
+      revert = rc != CLOUDSC_OK;
     }
   }
-  // the chosen buffers become the state's, the rest go back
+  // the chosen buffers become the state's and the originals they replace go
+  // (or, reverting, the other way round)
   for (int q = 0; q < n; q++) {
-    if (bf[members[q]] == sf[members[q]]) continue;
-    s->allocs.push_back(bf[members[q]]);
-    sf[members[q]] = bf[members[q]];
+    const int m = members[q];
+    if (bf[m] == sf[m]) continue;
+    if (revert) {
+      (void)hipFree(bf[m]);
+      continue;
+    }
+    dfree(s, sf[m]);
+    s->allocs.push_back(bf[m]);
+    sf[m] = bf[m];
   }
-  for (void* p : held) {
-    bool owned = false;
-    for (void* q : s->allocs) owned = owned || q == p;
-    if (owned) dfree(s, p); else (void)hipFree(p);
-  }
-  s->place_final_ms = best;
+  s->place_first_ms = cost.first_ms;
+  s->place_final_ms = cost.final_ms;
+  s->place_tries = cost.tries;
+  s->place_moves = cost.moves;
+  cost.search_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return rc;
 }
 
@@ -361,8 +296,9 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
 // (profiles/r04/placement/placement_search_ab_fp64.jsonl), so the pages its
 // inputs landed on are tried too.  Same rule: a set is kept when the kernel is
 // more than 1 % faster.  members/bytes: the input fields (positions in
-// cloudsc_fields_t); member -1 is the pristine plude copy.  Rejected sets are
-// held until the end, so a retry does not get the same pages back.
+// cloudsc_fields_t); member -1 is the pristine plude copy.  A rejected set is
+// freed as soon as it loses; the spacers, held to the end, keep the next
+// candidate off its pages.
 constexpr int kPlaceInputSets = 4;   // the first in field order, the others shuffled with spacers
 int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, int n) {
   float best = s->place_final_ms;
@@ -376,6 +312,11 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
   uint32_t rng = 0x85ebca6bu ^ (uint32_t)(uintptr_t)s;
   auto next = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
   int rc = CLOUDSC_OK;
+  PlaceCost& cost = s->pcost;
+  const auto t0 = std::chrono::steady_clock::now();
+  size_t live = 0;                        // candidate and spacer bytes held now
+  auto note = [&]() { cost.peak_bytes = std::max(cost.peak_bytes, (long long)live); };
+  std::vector<size_t> mine_bytes;
   for (int k = 0; k < kPlaceInputSets && rc == CLOUDSC_OK; k++) {
     cloudsc_fields_t cand = s->f;
     void* cand_pl = s->plude_pristine;
@@ -389,12 +330,18 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
       const int q = order[i];
       if (k > 0) {
         void* sp = nullptr;
-        if (hipMalloc(&sp, ((size_t)1 + next() % 16) << 21) != hipSuccess) { (void)hipGetLastError(); break; }
+        const size_t sb = ((size_t)1 + next() % 16) << 21;
+        if (hipMalloc(&sp, sb) != hipSuccess) { (void)hipGetLastError(); break; }
         spacers.push_back(sp);
+        live += sb;
+        note();
       }
       void* p = nullptr;
       if (hipMalloc(&p, bytes[q]) != hipSuccess) { (void)hipGetLastError(); break; }
       mine.push_back(p);
+      mine_bytes.push_back(bytes[q]);
+      live += bytes[q];
+      note();
       void*& src = slot(sf, s->plude_pristine, members[q]);
       if (hipMemcpyAsync(p, src, bytes[q], hipMemcpyDeviceToDevice, s->stream) != hipSuccess) {
         rc = CLOUDSC_EHIP;
@@ -405,9 +352,31 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
     }
     if (rc != CLOUDSC_OK || got < n) break;
     const float t = probe_kernel(s, cand, cand_pl);
+    cost.launches += 3;
     s->place_tries += n;
     if (t < 0.f) { rc = CLOUDSC_EHIP; break; }
-    if (t < best * 0.99f) { best = t; best_f = cand; best_pl = cand_pl; s->place_moves += n; }
+    // the set that loses -- this candidate, or the one it beats -- is freed
+    // at once (the transient footprint); the spacers, held to the
+    // end, keep the next candidate off its pages
+    cloudsc_fields_t lose_f = cand;
+    void* lose_pl = cand_pl;
+    if (t < best * 0.99f) {
+      lose_f = best_f; lose_pl = best_pl;
+      best = t; best_f = cand; best_pl = cand_pl; s->place_moves += n;
+    }
+    if (hipStreamSynchronize(s->stream) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
+    void** lf = (void**)&lose_f;
+    for (int q = 0; q < n; q++) {
+      void* p = slot(lf, lose_pl, members[q]);
+      for (size_t j = 0; j < mine.size(); j++)
+        if (mine[j] == p) {       // a candidate of this search (not one of the state's own buffers)
+          (void)hipFree(p);
+          live -= mine_bytes[j];
+          mine[j] = mine.back(); mine.pop_back();
+          mine_bytes[j] = mine_bytes.back(); mine_bytes.pop_back();
+          break;
+        }
+    }
   }
   if (hipStreamSynchronize(s->stream) != hipSuccess && rc == CLOUDSC_OK) rc = CLOUDSC_EHIP;
   for (void* p : spacers) (void)hipFree(p);
@@ -433,6 +402,7 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
     if (!kept) (void)hipFree(p);
   }
   if (rc == CLOUDSC_OK) s->place_final_ms = best;
+  cost.search_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return rc;
 }
 
@@ -562,9 +532,14 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
     if (hipMemsetAsync(s->kseg_ws, 0, 256, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);
     constexpr int no = (int)(sizeof(outs) / sizeof(outs[0]));
     int members[no];
-    size_t bytes[no];
-    for (int q = 0; q < no; q++) { members[q] = member(outs[q].dst); bytes[q] = outs[q].bytes; }
-    if ((rc = place_outputs(s, members, bytes, no))) return fail(rc);
+    size_t bytes[no], out_set = 0, in_set = 0;
+    for (int q = 0; q < no; q++) { members[q] = member(outs[q].dst); bytes[q] = outs[q].bytes; out_set += bytes[q]; }
+    for (const In& in : ins)
+      if (in.src) in_set += in.bytes;
+    // no room for two candidate sets and their spacers next to the state: no
+    // search (cloudsc_state_placement_report then says NONE)
+    const bool room = search_fits(2 * std::max(out_set, in_set) + ((size_t)64 << 25));
+    if (room && (rc = place_outputs(s, members, bytes, no))) return fail(rc);
     // then the inputs (contents copied) and the pristine plude copy
     constexpr int ni = (int)(sizeof(ins) / sizeof(ins[0]));
     int imem[ni];
@@ -575,7 +550,7 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
       imem[nin] = in.dst == (const void**)&plude_dev ? -1 : member(in.dst);
       ibytes[nin++] = in.bytes;
     }
-    if ((rc = place_inputs(s, imem, ibytes, nin))) return fail(rc);
+    if (room && (rc = place_inputs(s, imem, ibytes, nin))) return fail(rc);
   }
   for (Out& o : outs)
     if (hipMemsetAsync(*o.dst, 0xff, o.bytes, s->stream) != hipSuccess) return fail(CLOUDSC_EHIP);  // NaN
@@ -622,11 +597,27 @@ int cloudsc_state_placement(const cloudsc_gpu_state_t* s, float* probe_first_ms,
   return CLOUDSC_OK;
 }
 
-int cloudsc_debug_set_placement_search(int passes) {
+int cloudsc_state_placement_report(const cloudsc_gpu_state_t* s, cloudsc_placement_t* r) {
+  if (!s || !r) return CLOUDSC_EINVAL;
+  std::memset(r, 0, sizeof(*r));
+  r->probe_first_ms = s->place_first_ms;
+  r->probe_final_ms = s->place_final_ms;
+  r->tries = s->place_tries;
+  r->moves = s->place_moves;
+  r->launches = s->pcost.launches;
+  r->search_ms = s->pcost.search_ms;
+  r->peak_transient_bytes = s->pcost.peak_bytes;
+  r->method = s->pcost.launches ? CLOUDSC_PLACE_METHOD_KERNEL : CLOUDSC_PLACE_METHOD_NONE;
+  return CLOUDSC_OK;
+}
+
+int cloudsc_set_placement_search(int passes) {
   if (passes > 8) return CLOUDSC_EINVAL;
   g_place_passes.store(passes < 0 ? 2 : passes);
   return CLOUDSC_OK;
 }
+
+int cloudsc_debug_set_placement_search(int passes) { return cloudsc_set_placement_search(passes); }
 
 int cloudsc_debug_state_relocate_field(cloudsc_gpu_state_t* s, int member) {
   const int nmem = (int)(sizeof(s->fbytes) / sizeof(s->fbytes[0]));

@@ -55,6 +55,7 @@
 typedef struct {
   int numomp, ngptot, nproma, ngpus, precision, variant, reps, warmup;
   int transfer, chunk_blocks, nstreams, exact_libm;
+  int place;                      /* placement search: 1 on, 0 off, -1 auto (on when reps > 1) */
   double tol;
   int tol_given;
   const char *input_h5, *reference_h5, *data_dir, *write_h5_dir;
@@ -73,6 +74,7 @@ typedef struct {
   char err[256];                  /* this shard's cloudsc_last_hip_error() (thread-local in the library) */
   double t_start, t_end;          /* seconds, CLOCK_MONOTONIC */
   float *kernel_ms;
+  cloudsc_placement_t place;      /* the state's placement search and its cost */
   cloudsc_stats_t stats[CLOUDSC_NVALID];
 } shard_t;
 
@@ -102,6 +104,8 @@ static void usage(const char *prog) {
           "  --fp32-exact-libm     fp32: exp/pow with the glibc algorithms (bit-identical to the fp32\n"
           "                        restatement) instead of the default float-internal device forms\n"
           "  --reps R              timed steps (default 1)\n"
+          "  --place on|off|auto   output placement search at state creation (~0.5 s, ~250 kernel\n"
+          "                        launches; default auto: on when --reps > 1, off for one step)\n"
           "  --warmup W            untimed steps before the timed ones (default 1)\n"
           "  --input FILE          input HDF5 file (default ./input.h5 when present)\n"
           "  --reference FILE      reference HDF5 file (default ./reference.h5 when present)\n"
@@ -121,7 +125,7 @@ static int parse(int argc, char **argv, options_t *o) {
   memset(o, 0, sizeof(*o));
   o->numomp = 1; o->ngptot = 100; o->nproma = 4;     /* dwarf_cloudsc.c:25-27 defaults */
   o->ngpus = 1; o->precision = CLOUDSC_FP64; o->variant = CLOUDSC_VARIANT_KSEG;
-  o->reps = 1; o->warmup = 1; o->tol = 10.0 * DBL_EPSILON;
+  o->reps = 1; o->warmup = 1; o->tol = 10.0 * DBL_EPSILON; o->place = -1;
   o->chunk_blocks = 128; o->nstreams = 3;  /* chunk slots; profiles/r04/transfer_sweep_kseg_fp64.txt */
   int npos = 0;
   long pos[3] = {0, 0, 0};
@@ -145,6 +149,13 @@ static int parse(int argc, char **argv, options_t *o) {
       else { fprintf(stderr, "bad variant %s\n", v); return -1; }
     } else if (!strcmp(a, "--reps")) { NEEDV(); o->reps = atoi(v); }
     else if (!strcmp(a, "--warmup")) { NEEDV(); o->warmup = atoi(v); }
+    else if (!strcmp(a, "--place")) {
+      NEEDV();
+      if (!strcmp(v, "on")) o->place = 1;
+      else if (!strcmp(v, "off")) o->place = 0;
+      else if (!strcmp(v, "auto")) o->place = -1;
+      else { fprintf(stderr, "bad --place %s\n", v); return -1; }
+    }
     else if (!strcmp(a, "--input")) { NEEDV(); o->input_h5 = v; }
     else if (!strcmp(a, "--reference")) { NEEDV(); o->reference_h5 = v; }
     else if (!strcmp(a, "--data")) { NEEDV(); o->data_dir = v; }
@@ -204,6 +215,7 @@ static void *shard_main(void *arg) {
   cloudsc_gpu_state_t *st = NULL;
   s->rc = cloudsc_state_create(&st, s->device, s->precision, s->ngptot, s->nproma, s->col_offset, s->tmpl,
                                s->params);
+  if (!s->rc) s->rc = cloudsc_state_placement_report(st, &s->place);
   if (!s->rc && s->warmup > 0) {
     float *w = (float *)malloc(sizeof(float) * s->warmup);
     s->rc = w ? cloudsc_state_run(st, s->variant | s->libm_bit, s->warmup, w) : CLOUDSC_ENOMEM;
@@ -460,6 +472,12 @@ int main(int argc, char **argv) {
          variant_name(o.variant),
          o.ngpus, ds.source, ds.klon, ds.klev);
 
+  /* the placement search costs ~0.5 s of kernel launches per state and saves
+   * up to ~15 % per step: worth it for repeated steps, not for one (the
+   * reference times a single launch, cloudsc_driver.cu:389-422) */
+  const int place = o.place >= 0 ? o.place : o.reps > 1;
+  cloudsc_set_placement_search(place ? -1 : 0);
+
   /* ---- shard: block-aligned contiguous ranges of the global column index ---- */
   shard_t *sh = (shard_t *)calloc((size_t)o.ngpus, sizeof(shard_t));
   pthread_t *th = (pthread_t *)calloc((size_t)o.ngpus, sizeof(pthread_t));
@@ -535,6 +553,17 @@ int main(int argc, char **argv) {
   }
   printf(" TIMING: steps=%d wall_ms_per_step=%.4f kernel_ms_per_step=%.4f columns_per_s=%.1f devices=%d\n", o.reps,
          1e3 * tdiff / o.reps, kmax, cols_done / tdiff, nused);
+  /* the placement search of each shard's state (cloudsc_state_placement_report) */
+  for (int d = 0; d < nused; d++) {
+    const cloudsc_placement_t *pl = &sh[d].place;
+    if (pl->method == CLOUDSC_PLACE_METHOD_NONE) {
+      printf(" PLACEMENT: shard=%d search=off\n", d);
+      continue;
+    }
+    printf(" PLACEMENT: shard=%d search=kernel first_ms=%.4f kept_ms=%.4f tries=%d moves=%d launches=%d "
+           "search_ms=%.1f peak_transient_MB=%.1f\n", d, pl->probe_first_ms, pl->probe_final_ms, pl->tries,
+           pl->moves, pl->launches, pl->search_ms, pl->peak_transient_bytes / 1048576.0);
+  }
 
   /* ---- validation (cloudsc_validate.c:193-216, combined over devices) ---- */
   int bad = 0;

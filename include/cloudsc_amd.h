@@ -181,6 +181,51 @@ int cloudsc_gpu_run(int device, void *stream, int precision, int variant,
                     int ngptot, int nproma, int klev,
                     const cloudsc_fields_t *device_fields, void *scratch);
 
+/* ------------------------------------------------------------------------ */
+/* Caller-owned device fields, placed (round 5)                              */
+/* ------------------------------------------------------------------------ */
+/* How fast the kernel writes its 21 output fields depends on where they land
+ * in HBM: field sets of one configuration ran the fp64 KSEG kernel at
+ * 1.63-1.94 ms, and the slow ones stall on DRAM write credits (DESIGN.md
+ * §3.12).  A placement search allocates candidate buffers, times a probe over
+ * them and keeps a candidate when the probe is > 1 % faster.  Its cost and
+ * result: */
+typedef struct cloudsc_placement {
+  float probe_first_ms, probe_final_ms;   /* probe time of the first / the kept placement            */
+  int tries, moves;                       /* candidate buffers allocated / kept                      */
+  int launches;                           /* probe launches run (untimed warm-ups included)          */
+  int method;                             /* CLOUDSC_PLACE_METHOD_*                                  */
+  double search_ms;                       /* wall time of the search                                 */
+  long long peak_transient_bytes;         /* most device bytes held at once beyond the fields' own   */
+} cloudsc_placement_t;
+#define CLOUDSC_PLACE_METHOD_NONE        0   /* no search                                             */
+#define CLOUDSC_PLACE_METHOD_KERNEL      1   /* the KSEG kernel on the state's own inputs (state API)  */
+#define CLOUDSC_PLACE_METHOD_WRITE_PROBE 2   /* the kernel's output write pattern, no physics          */
+
+/* cloudsc_fields_alloc flags */
+#define CLOUDSC_PLACE_NONE     1   /* one allocation per field, no search (a caller that runs one step) */
+#define CLOUDSC_ALLOC_AEROSOLS 2   /* also allocate the five aerosol inputs (LAERICESED/LAERICEAUTO)     */
+
+/* Allocate the device buffers of every field of an (ngptot, nproma, klev,
+ * precision) problem on `device` -- one allocation per field, block layout, as
+ * the reference GPU driver's cudaMalloc calls do (cloudsc_driver.cu:276-328) --
+ * for the caller to fill and to run with cloudsc_gpu_run.  Unless flags has
+ * CLOUDSC_PLACE_NONE, the output buffers (plude included) are then placed by a
+ * search timed with the kernel's output write pattern (no physics, no field
+ * contents needed: the caller fills the inputs afterwards): 8 whole fresh
+ * output sets, then up to two passes of one field at a time
+ * (csrc/cloudsc_place.hip).  The search overwrites nothing the caller owns.
+ * Input buffers are never moved (their placement does not change the kernel
+ * time).  `report` (may be NULL) receives the search's cost and result.  On an
+ * error nothing stays allocated. */
+int cloudsc_fields_alloc(int device, int precision, int ngptot, int nproma, int klev, int flags,
+                         cloudsc_fields_t *fields, cloudsc_placement_t *report);
+
+/* Free the buffers cloudsc_fields_alloc made and set their pointers to NULL.
+ * Non-NULL pointers it did not make (on this device) are left alone and make
+ * the call return CLOUDSC_EINVAL. */
+int cloudsc_fields_free(int device, cloudsc_fields_t *fields);
+
 /* Bytes of device scratch a variant needs for (ngptot, nproma, klev, precision); 0 for KCACHE. */
 long long cloudsc_gpu_scratch_bytes(int precision, int variant, int ngptot, int nproma, int klev);
 
@@ -348,21 +393,44 @@ int cloudsc_state_fields(const cloudsc_gpu_state_t *state, cloudsc_fields_t *out
  * (fp64 KSEG 1.63-1.94 ms for states of one configuration: fields written
  * together whose physical pages collide stall on DRAM write credits).  At
  * creation the state times the KSEG kernel on its own inputs over candidate
- * placements of its outputs -- whole fresh output sets, then one field at a
- * time -- then of its inputs (two whole fresh input sets, contents copied),
- * and keeps a candidate when the time drops by more than 1 %.
+ * placements of its outputs -- eight whole fresh output sets (the last seven
+ * shuffled with spacers), then one field at a time -- then of its inputs
+ * (four whole fresh input sets, the last three shuffled with spacers,
+ * contents copied), and keeps a candidate when the time drops by more than
+ * 1 %.  Each rejected input set is freed as soon as it loses.
  * If the search's launches time out in a segment hand-off, the first
  * placement is kept and probe_final_ms is negative (the state is created).
  * probe_first_ms / probe_final_ms: the kernel time of the first / the kept
- * placement, tries / moves: output buffers allocated as candidates / kept.
+ * placement, tries / moves: buffers (outputs and inputs) allocated as
+ * candidates / kept.  Cost (wall time, launches, transient bytes):
+ * cloudsc_state_placement_report.
  * All zero when the search was off.  Any pointer may be NULL. */
 int cloudsc_state_placement(const cloudsc_gpu_state_t *state, float *probe_first_ms, float *probe_final_ms,
                             int *tries, int *moves);
 
-/* Diagnostic: passes of the output placement search of the states created
- * after this call (0 = off: the first allocation is kept; negative = the
- * default, 2; at most 8).  The results do not depend on it. */
+/* The placement search of the state (cloudsc_state_placement) with its cost:
+ * all of it, outputs and inputs, method CLOUDSC_PLACE_METHOD_KERNEL, or
+ * CLOUDSC_PLACE_METHOD_NONE with zeros when the search was off. */
+int cloudsc_state_placement_report(const cloudsc_gpu_state_t *state, cloudsc_placement_t *report);
+
+/* Passes of the output placement search of the states created after this
+ * call, process-wide (0 = off: the first allocation is kept; negative = the
+ * default, 2; at most 8).  The results do not depend on it; the search costs
+ * ~0.5 s of kernel launches per fp64 state at NGPTOT=163840 and pays off only
+ * over many steps (the CLI turns it off for one step). */
+int cloudsc_set_placement_search(int passes);
+/* The same (the name of rounds 3-4). */
 int cloudsc_debug_set_placement_search(int passes);
+
+/* Measurement: the memory-pattern probe (csrc/cloudsc_place.hip) over the
+ * device fields f: one wave per 64-column sub-block streams the level planes
+ * the way the KSEG kernel does, with no physics.  mode 0 writes every non-NULL
+ * output field; mode 1 also reads every input field.  *ms = best of `reps`
+ * timed launches after one untimed.  Outputs (plude included) are
+ * overwritten with junk; input contents do not matter.  It ranks placements
+ * of a field set without its contents (tools/place_corr.py). */
+int cloudsc_debug_memory_probe(int device, int precision, int ngptot, int nproma, int klev,
+                               const cloudsc_fields_t *f, int mode, int reps, float *ms);
 
 /* Diagnostic: move field `member` (its position in cloudsc_fields_t) of a state
  * to a new device allocation, contents copied; the old allocation is kept until

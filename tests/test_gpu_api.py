@@ -387,3 +387,84 @@ def test_kseg_shared_workspace_alternating_states(lib, ds, precision):
             hip.hipFree(ws)
         for g in states:
             g.close()
+
+
+# ---- caller-owned device fields with a placement search (cloudsc_fields_alloc, round 5) ----
+def device_outputs(df, ngptot):
+    return {k: ca.blocks_to_columns(df.download(k), ngptot) for _, k in ca.VALIDATED}
+
+
+@pytest.mark.parametrize("precision,variant", [(ca.FP64, ca.VARIANT_KSEG), (ca.FP64, ca.VARIANT_KCACHE),
+                                               (ca.FP32, ca.VARIANT_KSEG)])
+def test_fields_alloc_reference_driver_shape(lib, ds, precision, variant):
+    """The reference CUDA driver's shape on caller-owned buffers: allocate every
+    field (cloudsc_fields_alloc, placed by the write-pattern search), copy the
+    host block-layout inputs in, cloudsc_gpu_run, copy the outputs out -- bit
+    for bit what the state API computes.  The search's record is consistent,
+    and cloudsc_fields_free releases every buffer it made."""
+    ngptot, nproma = 3000, 64
+    ref = outputs_of_state(ds, ngptot, nproma, precision, variant)
+    df = ca.DeviceFields(ngptot, nproma, ds.klev, precision)
+    ws = C.c_void_p()
+    hip = C.CDLL("libamdhip64.so.7")
+    try:
+        r = df.report.to_dict()
+        assert r["method"] == "write-probe" and r["launches"] >= 30 and r["search_ms"] > 0, r
+        assert 0 < r["probe_final_ms"] <= r["probe_first_ms"] and 0 <= r["moves"] <= r["tries"], r
+        assert r["tries"] >= 21 and r["peak_transient_bytes"] > 0, r
+        # every field allocated, aerosols only on request
+        assert all(getattr(df.f, n) for n in list(ca.INPUT_FIELDS) + list(ca.OUTPUT_FIELDS) + ["plude"])
+        assert not any(getattr(df.f, n) for n in ca.AEROSOL_FIELDS)
+        st = ca.make_host_state(ds, ngptot, nproma, precision)
+        df.upload({k: v for k, v in st.arrays.items() if k in ca.INPUT_FIELDS or k == "plude"})
+        p = ca.Params.from_dict(ds.params)
+        ca.check(lib.cloudsc_gpu_init(0, C.byref(p)))
+        nbytes = lib.cloudsc_gpu_scratch_bytes(precision, variant, ngptot, nproma, ds.klev)
+        if nbytes > 0:
+            assert hip.hipMalloc(C.byref(ws), C.c_size_t(nbytes)) == 0
+            assert hip.hipMemset(ws, 0, C.c_size_t(256)) == 0
+        ca.check(lib.cloudsc_gpu_run(0, None, precision, variant, ngptot, nproma, ds.klev, C.byref(df.f), ws))
+        ca.check(lib.cloudsc_gpu_check(0, None, variant, ws))
+        assert bitwise_mismatches(device_outputs(df, ngptot), ref) == {}
+    finally:
+        if ws.value:
+            hip.hipFree(ws)
+        df.close()
+    assert df.f is None
+
+
+def outputs_of_state(ds, ngptot, nproma, precision, variant):
+    g = ca.GpuState(ds, ngptot, nproma, precision)
+    try:
+        return outputs_of(g, variant)
+    finally:
+        g.close()
+
+
+def test_fields_alloc_flags_and_free(lib, ds):
+    """CLOUDSC_PLACE_NONE: no search, record zero; CLOUDSC_ALLOC_AEROSOLS
+    allocates the five aerosol inputs; unknown flags and foreign pointers are
+    refused; a state reports its own search with its cost."""
+    f, r = ca.Fields(), ca.Placement()
+    assert lib.cloudsc_fields_alloc(0, ca.FP64, 1000, 128, ds.klev, 4, C.byref(f), C.byref(r)) == ca.EINVAL
+    ca.check(lib.cloudsc_fields_alloc(0, ca.FP64, 1000, 128, ds.klev, ca.PLACE_NONE | ca.ALLOC_AEROSOLS,
+                                      C.byref(f), C.byref(r)))
+    try:
+        assert r.to_dict()["method"] == "none" and r.launches == 0 and r.tries == 0
+        assert all(getattr(f, n) for n in ca.AEROSOL_FIELDS)
+        own = f.pt
+        g = ca.GpuState(ds, 1000, 128)
+        try:
+            foreign = ca.Fields()
+            ca.check(lib.cloudsc_state_fields(g.h, C.byref(foreign)))
+            f2 = ca.Fields(pt=foreign.pt)
+            assert lib.cloudsc_fields_free(0, C.byref(f2)) == ca.EINVAL and f2.pt == foreign.pt
+            rep = g.placement_report()
+            assert rep["method"] == "kernel" and rep["launches"] > 0 and rep["search_ms"] > 0, rep
+            assert rep["peak_transient_bytes"] > 0, rep
+        finally:
+            g.close()
+        assert own
+    finally:
+        ca.check(lib.cloudsc_fields_free(0, C.byref(f)))
+    assert not f.pt and not f.pfhpsn

@@ -28,7 +28,7 @@ def main():
         open(p, "w").write(s.replace(old, new))
     out = os.path.join(REPO, "build", "lib%s.so" % name)
     srcs = [os.path.join(tmp, "csrc", f) for f in ("cloudsc_gpu.hip", "cloudsc_state.hip", "cloudsc_pipeline.hip",
-                                                     "cloudsc_cpu.hip", "cloudsc_hbm.hip")]
+                                                     "cloudsc_cpu.hip", "cloudsc_hbm.hip", "cloudsc_place.hip")]
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-ffp-contract=off", "-fPIC", "-std=c++17", "--offload-arch=gfx950",
            "-Wno-unused-result", "-mllvm", "-disable-machine-licm", "-Xarch_host", "-mfma",
            "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(tmp, "csrc"), "-shared"] + extra + srcs + \
