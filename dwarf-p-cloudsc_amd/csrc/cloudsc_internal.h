@@ -126,6 +126,14 @@ struct PlaceCost {
 int search_outputs(cloudsc_fields_t& f, const int* members, const size_t* bytes, int n, int sets, int passes,
                    uint32_t seed, const std::function<float(const cloudsc_fields_t&)>& probe, PlaceCost& cost);
 
+// Device allocations of the state and the placement searches.  Plain
+// hipMalloc / hipExtMallocWithFlags + hipFree; in the diagnostic build
+// -DCLOUDSC_DEBUG_CANARY every buffer gets a 64 KiB guard band of a known byte
+// on each side, checked by cloudsc_debug_canary_check and at free (the
+// round-5 record of the contiguous-allocation failure).
+hipError_t dev_malloc(void** p, size_t bytes, unsigned flags = 0);
+void dev_free(void* p);
+
 // whether a placement search whose candidates peak at about `transient` bytes
 // fits the device's free memory with room to spare (on a device
 // shared by several ranks the search must not starve their allocations)

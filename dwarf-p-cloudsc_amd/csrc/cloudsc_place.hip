@@ -176,6 +176,65 @@ int memory_probe(int device, hipStream_t stream, int precision, int ngptot, int 
   return CLOUDSC_OK;
 }
 
+#ifndef CLOUDSC_DEBUG_CANARY
+hipError_t dev_malloc(void** p, size_t bytes, unsigned flags) {
+  return flags ? hipExtMallocWithFlags(p, bytes, flags) : hipMalloc(p, bytes);
+}
+void dev_free(void* p) { (void)hipFree(p); }
+#else
+// Diagnostic build: a 64 KiB guard band of kCanaryByte on each side of every
+// buffer.  Live buffers are registered; cloudsc_debug_canary_check reads every
+// band back, dev_free checks a buffer's bands before it goes.
+constexpr size_t kGuard = (size_t)64 << 10;
+constexpr unsigned char kCanaryByte = 0xC3;
+struct Guarded { char* base; size_t bytes; };
+std::mutex g_canary_mu;
+std::unordered_map<void*, Guarded> g_canary;          // user pointer -> allocation
+long long g_canary_bad_at_free = 0;                   // guard bytes found changed when a buffer was freed
+long long guard_bad_bytes(const Guarded& g) {
+  std::vector<unsigned char> h(kGuard);
+  long long bad = 0;
+  for (const char* band : {g.base, g.base + kGuard + g.bytes}) {
+    if (hipMemcpy(h.data(), band, kGuard, hipMemcpyDeviceToHost) != hipSuccess) { (void)hipGetLastError(); return -1; }
+    for (unsigned char c : h) bad += c != kCanaryByte;
+  }
+  return bad;
+}
+hipError_t dev_malloc(void** p, size_t bytes, unsigned flags) {
+  char* base = nullptr;
+  const size_t total = bytes + 2 * kGuard;
+  hipError_t e = flags ? hipExtMallocWithFlags((void**)&base, total, flags) : hipMalloc((void**)&base, total);
+  if (e != hipSuccess) return e;
+  if ((e = hipMemset(base, kCanaryByte, kGuard)) != hipSuccess ||
+      (e = hipMemset(base + kGuard + bytes, kCanaryByte, kGuard)) != hipSuccess ||
+      (e = hipDeviceSynchronize()) != hipSuccess) {
+    (void)hipFree(base);
+    return e;
+  }
+  *p = base + kGuard;
+  std::lock_guard<std::mutex> lk(g_canary_mu);
+  g_canary[*p] = Guarded{base, bytes};
+  return hipSuccess;
+}
+void dev_free(void* p) {
+  Guarded g{nullptr, 0};
+  {
+    std::lock_guard<std::mutex> lk(g_canary_mu);
+    auto it = g_canary.find(p);
+    if (it == g_canary.end()) { (void)hipFree(p); return; }
+    g = it->second;
+    g_canary.erase(it);
+  }
+  (void)hipDeviceSynchronize();
+  const long long bad = guard_bad_bytes(g);
+  if (bad > 0) {
+    std::lock_guard<std::mutex> lk(g_canary_mu);
+    g_canary_bad_at_free += bad;
+  }
+  (void)hipFree(g.base);
+}
+#endif
+
 bool search_fits(size_t transient) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) { (void)hipGetLastError(); return false; }
@@ -207,12 +266,12 @@ int search_outputs(cloudsc_fields_t& f, const int* members, const size_t* bytes,
   bool room = true;
   auto fresh = [&](size_t nb) -> void* {
     void* q = nullptr;
-    if (!room || hipMalloc(&q, nb) != hipSuccess) { (void)hipGetLastError(); room = false; return nullptr; }
+    if (!room || dev_malloc(&q, nb) != hipSuccess) { (void)hipGetLastError(); room = false; return nullptr; }
     live += nb;
     note();
     return q;
   };
-  auto drop = [&](void* p, size_t nb) { (void)hipFree(p); live -= nb; };
+  auto drop = [&](void* p, size_t nb) { dev_free(p); live -= nb; };
   auto is_orig = [&](int q) { return bf[members[q]] == of[members[q]]; };
   float best = probe(f);
   if (best < 0.f) return CLOUDSC_EHIP;
@@ -355,7 +414,7 @@ extern "C" int cloudsc_fields_alloc(int device, int precision, int ngptot, int n
   for (int m = 0; m < kNumFields; m++) {
     if (kFieldTable[m].dir == FD_AEROSOL && !(flags & CLOUDSC_ALLOC_AEROSOLS)) continue;
     void* p = nullptr;
-    const hipError_t e = hipMalloc(&p, member_bytes(m, precision, ngptot, nproma, klev));
+    const hipError_t e = dev_malloc(&p, member_bytes(m, precision, ngptot, nproma, klev));
     if (e != hipSuccess) {
       hip_fail(e, "hipMalloc");
       cloudsc_fields_free(device, out);
@@ -407,7 +466,7 @@ extern "C" int cloudsc_fields_alloc(int device, int precision, int ngptot, int n
     if (rc) df[m] = bf[m];
     else fields_register(df[m], device);
     if (!rc) fields_unregister(bf[m], device);
-    (void)hipFree(drop);
+    dev_free(drop);
   }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
@@ -437,11 +496,61 @@ extern "C" int cloudsc_fields_free(int device, cloudsc_fields_t* f) {
   for (int m = 0; m < kNumFields; m++) {
     if (!df[m]) continue;
     if (fields_unregister(df[m], device)) {
-      (void)hipFree(df[m]);
+      dev_free(df[m]);
       df[m] = nullptr;
     } else {
       rc = CLOUDSC_EINVAL;   // not a buffer of cloudsc_fields_alloc on this device: left alone
     }
   }
   return rc;
+}
+
+// Diagnostic: guard bands of the live buffers (CLOUDSC_DEBUG_CANARY builds;
+// elsewhere CLOUDSC_EINVAL).  *live = guarded buffers alive, *bad_allocs = of
+// them with a changed guard byte, *bad_bytes = changed guard bytes in all of
+// them plus those found at free since the last call (which clears that count).
+extern "C" int cloudsc_debug_canary_check(int* live, int* bad_allocs, long long* bad_bytes) {
+#ifndef CLOUDSC_DEBUG_CANARY
+  (void)live; (void)bad_allocs; (void)bad_bytes;
+  return CLOUDSC_EINVAL;
+#else
+  if (!live || !bad_allocs || !bad_bytes) return CLOUDSC_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  std::vector<Guarded> all;
+  long long at_free;
+  {
+    std::lock_guard<std::mutex> lk(g_canary_mu);
+    for (auto& kv : g_canary) all.push_back(kv.second);
+    at_free = g_canary_bad_at_free;
+    g_canary_bad_at_free = 0;
+  }
+  *live = (int)all.size();
+  *bad_allocs = 0;
+  *bad_bytes = at_free;
+  for (const Guarded& g : all) {
+    const long long b = guard_bad_bytes(g);
+    if (b < 0) return CLOUDSC_EHIP;
+    if (b > 0) { (*bad_allocs)++; *bad_bytes += b; }
+  }
+  return CLOUDSC_OK;
+#endif
+}
+
+// Diagnostic: copy `bytes` (a multiple of 4) from src to dst with a kernel --
+// 4-byte vector loads and stores through the caches, a grid over all XCDs --
+// and wait; for comparing what the shader cores read with what a copy engine
+// (hipMemcpy) reads from the same memory.
+namespace {
+__global__ void __launch_bounds__(256) word_copy_kernel(unsigned* dst, const unsigned* src, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+}  // namespace
+extern "C" int cloudsc_debug_kernel_copy(void* dst, const void* src, long long bytes) {
+  if (!dst || !src || bytes <= 0 || bytes % 4) return CLOUDSC_EINVAL;
+  hipLaunchKernelGGL(word_copy_kernel, dim3(2048), dim3(256), 0, nullptr, (unsigned*)dst, (const unsigned*)src,
+                     (size_t)bytes / 4);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return CLOUDSC_OK;
 }

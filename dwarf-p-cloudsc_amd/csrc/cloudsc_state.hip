@@ -153,9 +153,9 @@ std::atomic<unsigned> g_alloc_flags{0};
 int dalloc(cloudsc_gpu_state* s, void** p, size_t bytes) {
 #ifdef CLOUDSC_DEBUG_KNOBS
   const unsigned fl = g_alloc_flags.load();
-  hipError_t e = fl ? hipExtMallocWithFlags(p, bytes, fl) : hipMalloc(p, bytes);
+  hipError_t e = dev_malloc(p, bytes, fl);
 #else
-  hipError_t e = hipMalloc(p, bytes);
+  hipError_t e = dev_malloc(p, bytes);
 #endif
   if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
   s->allocs.push_back(*p);
@@ -230,7 +230,7 @@ float probe_kernel(cloudsc_gpu_state* s, const cloudsc_fields_t& f, const void* 
 void dfree(cloudsc_gpu_state* s, void* p) {
   for (auto& q : s->allocs)
     if (q == p) { q = s->allocs.back(); s->allocs.pop_back(); break; }
-  (void)hipFree(p);
+  dev_free(p);
 }
 
 // members/bytes: the output fields (positions in cloudsc_fields_t); moves
@@ -276,7 +276,7 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
     const int m = members[q];
     if (bf[m] == sf[m]) continue;
     if (revert) {
-      (void)hipFree(bf[m]);
+      dev_free(bf[m]);
       continue;
     }
     dfree(s, sf[m]);
@@ -331,13 +331,13 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
       if (k > 0) {
         void* sp = nullptr;
         const size_t sb = ((size_t)1 + next() % 16) << 21;
-        if (hipMalloc(&sp, sb) != hipSuccess) { (void)hipGetLastError(); break; }
+        if (dev_malloc(&sp, sb) != hipSuccess) { (void)hipGetLastError(); break; }
         spacers.push_back(sp);
         live += sb;
         note();
       }
       void* p = nullptr;
-      if (hipMalloc(&p, bytes[q]) != hipSuccess) { (void)hipGetLastError(); break; }
+      if (dev_malloc(&p, bytes[q]) != hipSuccess) { (void)hipGetLastError(); break; }
       mine.push_back(p);
       mine_bytes.push_back(bytes[q]);
       live += bytes[q];
@@ -370,7 +370,7 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
       void* p = slot(lf, lose_pl, members[q]);
       for (size_t j = 0; j < mine.size(); j++)
         if (mine[j] == p) {       // a candidate of this search (not one of the state's own buffers)
-          (void)hipFree(p);
+          dev_free(p);
           live -= mine_bytes[j];
           mine[j] = mine.back(); mine.pop_back();
           mine_bytes[j] = mine_bytes.back(); mine_bytes.pop_back();
@@ -379,7 +379,7 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
     }
   }
   if (hipStreamSynchronize(s->stream) != hipSuccess && rc == CLOUDSC_OK) rc = CLOUDSC_EHIP;
-  for (void* p : spacers) (void)hipFree(p);
+  for (void* p : spacers) dev_free(p);
   // as for the outputs: hand-off timeouts in the probes keep the first placement
   if (rc == CLOUDSC_OK) {
     const int hc = kseg_check(s->device, s->stream, s->kseg_ws);
@@ -399,7 +399,7 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
   for (void* p : mine) {
     bool kept = false;
     for (void* q : s->allocs) kept = kept || q == p;
-    if (!kept) (void)hipFree(p);
+    if (!kept) dev_free(p);
   }
   if (rc == CLOUDSC_OK) s->place_final_ms = best;
   cost.search_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -410,7 +410,7 @@ int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, 
 int expand_into(cloudsc_gpu_state* s, void* dst, const void* host_src, int nlev, bool is_int) {
   const size_t src_bytes = (size_t)nlev * s->klon * (is_int ? sizeof(int) : sizeof(double));
   void* d_src = nullptr;
-  HIPCHK(hipMalloc(&d_src, src_bytes));
+  HIPCHK(dev_malloc(&d_src, src_bytes));
   hipError_t e = hipMemcpyAsync(d_src, host_src, src_bytes, hipMemcpyHostToDevice, s->stream);
   if (e == hipSuccess) {
     // 1-D grid, enough workgroups to fill the chip, the kernel strides the rest
@@ -429,7 +429,7 @@ int expand_into(cloudsc_gpu_state* s, void* dst, const void* host_src, int nlev,
     e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   }
-  (void)hipFree(d_src);
+  dev_free(d_src);
   if (e != hipSuccess) return hip_fail(e, "expand");
   return CLOUDSC_OK;
 }
@@ -798,7 +798,7 @@ int cloudsc_state_destroy(cloudsc_gpu_state_t* s) {
   if (!s) return CLOUDSC_OK;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  for (void* p : s->allocs) (void)hipFree(p);
+  for (void* p : s->allocs) dev_free(p);
   param_set_free(&s->params);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);

@@ -432,6 +432,21 @@ int cloudsc_debug_set_placement_search(int passes);
 int cloudsc_debug_memory_probe(int device, int precision, int ngptot, int nproma, int klev,
                                const cloudsc_fields_t *f, int mode, int reps, float *ms);
 
+/* Diagnostic, diagnostic build only (-DCLOUDSC_DEBUG_CANARY; otherwise
+ * CLOUDSC_EINVAL): every device buffer of the states and placement searches
+ * carries a 64 KiB guard band of a known byte on each side.  *live = guarded
+ * buffers alive, *bad_allocs = those with a changed guard byte, *bad_bytes =
+ * changed guard bytes in them plus those found when buffers were freed since
+ * the last call.  For the round-5 record of the contiguous-allocation failure
+ * (tools/contig_diag_r05.py). */
+int cloudsc_debug_canary_check(int *live, int *bad_allocs, long long *bad_bytes);
+
+/* Diagnostic: copy `bytes` (a multiple of 4) from device memory src to dst
+ * with a kernel (4-byte vector loads and stores through the caches, a grid
+ * over all XCDs), then wait -- to compare what the shader cores read with what
+ * a copy engine (hipMemcpy) reads from the same memory. */
+int cloudsc_debug_kernel_copy(void *dst, const void *src, long long bytes);
+
 /* Diagnostic: move field `member` (its position in cloudsc_fields_t) of a state
  * to a new device allocation, contents copied; the old allocation is kept until
  * the state is destroyed, so the field lands on other physical pages.  For
