@@ -170,3 +170,82 @@ extern "C" int cloudsc_pcie_gbps(int device, long long bytes, int reps, double* 
   *both = best[2];
   return CLOUDSC_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Counter calibration (round 5): MI355X_MICROARCH.md
+// calibrates rocprofv3's FETCH_SIZE (x2) and WRITE_SIZE (x1) only for 16-byte
+// per-lane streaming accesses.  The CLOUDSC kernels load and store 8 bytes
+// (fp64) or 4 bytes (fp32) per lane, non-temporal, one 512 / 256-byte row per
+// wave instruction.  This streams a known byte count with exactly that access
+// shape -- a read of `bytes` (mode 0) or a write of `bytes` (mode 1), `width`
+// bytes per lane, consecutive lanes on consecutive elements, a grid striding
+// over the buffer -- so a PMC pass over it gives the counters' factor for the
+// kernels' own widths (tools/calib_counters.py).
+namespace {
+template <typename T, bool WRITE>
+__global__ void __launch_bounds__(256) stream_probe(T* __restrict__ a, size_t n, unsigned* __restrict__ sink) {
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, step = (size_t)gridDim.x * blockDim.x;
+  if constexpr (WRITE) {
+    for (size_t i = i0; i < n; i += step) {
+      T v;
+      if constexpr (sizeof(T) == 16) v = T{(unsigned)i, 0u, 0u, 0u};
+      else v = (T)i;
+      __builtin_nontemporal_store(v, a + i);
+    }
+  } else {
+    T acc{};
+    for (size_t i = i0; i < n; i += step) acc += __builtin_nontemporal_load(a + i);
+    bool hit;
+    if constexpr (sizeof(T) == 16) hit = acc.x == 1u;
+    else hit = acc == (T)1;
+    if (hit) sink[0] = 1;   // keeps the loads; never true for the zero-filled buffer
+  }
+}
+}  // namespace
+
+extern "C" int cloudsc_debug_stream_probe(int device, int mode, int width, long long bytes, int reps, double* ms) {
+  if (!ms || (mode != 0 && mode != 1) || (width != 4 && width != 8 && width != 16) || bytes < (1 << 20) ||
+      bytes % 16 || reps <= 0)
+    return CLOUDSC_EINVAL;
+  HIPCHK(hipSetDevice(device));
+  void* a = nullptr;
+  unsigned* sink = nullptr;
+  HIPCHK(hipMalloc(&a, (size_t)bytes));
+  hipError_t e = hipMalloc((void**)&sink, 64);
+  if (e == hipSuccess) e = hipMemset(a, 0, (size_t)bytes);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  double best = 0.0;
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+  for (int r = 0; r < reps && e == hipSuccess; r++) {
+    e = hipEventRecord(e0, nullptr);
+    const dim3 g(2048), b(256);
+    const size_t n = (size_t)bytes / width;
+    if (e == hipSuccess) {
+      if (width == 4) {
+        if (mode) hipLaunchKernelGGL((stream_probe<float, true>), g, b, 0, nullptr, (float*)a, n, sink);
+        else hipLaunchKernelGGL((stream_probe<float, false>), g, b, 0, nullptr, (float*)a, n, sink);
+      } else if (width == 8) {
+        if (mode) hipLaunchKernelGGL((stream_probe<double, true>), g, b, 0, nullptr, (double*)a, n, sink);
+        else hipLaunchKernelGGL((stream_probe<double, false>), g, b, 0, nullptr, (double*)a, n, sink);
+      } else {
+        if (mode) hipLaunchKernelGGL((stream_probe<u32x4v, true>), g, b, 0, nullptr, (u32x4v*)a, n, sink);
+        else hipLaunchKernelGGL((stream_probe<u32x4v, false>), g, b, 0, nullptr, (u32x4v*)a, n, sink);
+      }
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+    if (e == hipSuccess && (best == 0.0 || t < best)) best = t;
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(sink);
+  (void)hipFree(a);
+  if (e != hipSuccess) return hip_fail(e, "stream probe");
+  *ms = best;
+  return CLOUDSC_OK;
+}

@@ -287,6 +287,14 @@ int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, double *gbps);
  * bench.py reports pcie_inclusive against it. */
 int cloudsc_pcie_gbps(int device, long long bytes, int reps, double *h2d, double *d2h, double *both);
 
+/* Measurement: stream `bytes` (>= 1 MiB, a multiple of 16) through one device
+ * buffer with `width` (4, 8 or 16) bytes per lane per access, non-temporal,
+ * consecutive lanes on consecutive elements -- the CLOUDSC kernels' access
+ * shape at width 8 (fp64) and 4 (fp32) -- as a read (mode 0) or a write
+ * (mode 1); *ms = the fastest of `reps` launches.  A rocprofv3 PMC pass over it
+ * calibrates FETCH_SIZE / WRITE_SIZE for those widths (tools/calib_counters.py). */
+int cloudsc_debug_stream_probe(int device, int mode, int width, long long bytes, int reps, double *ms);
+
 /* ABI introspection for bindings: sizeof of the public structs
  * (0 params, 1 fields, 2 template, 3 reference, 4 stats), -1 otherwise. */
 long long cloudsc_abi_sizeof(int which);

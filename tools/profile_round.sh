@@ -27,6 +27,20 @@ d.update(json.load(open(src)))
 json.dump(d, open(dst, "w"), indent=1, sort_keys=True)
 PY
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/stats_${variant}_${prec} -o bench --output-format csv \
-  -- python3 $R/bench.py --steps 100 --warmup 5 --no-transfer --variant $variant --precision $prec --nproma $nproma \
-  > $out/bench_under_rocprof_${variant}_${prec}.log 2>&1 || exit $?
+  -- python3 $R/bench.py --steps 100 --warmup 5 --no-transfer --no-cpu-baseline --variant $variant --precision $prec \
+  --nproma $nproma > $out/bench_under_rocprof_${variant}_${prec}.log 2>&1 || exit $?
+# the --stats summary averages every launch of the kernel (placement probes, first step, prewarm, energy
+# window); the timed launches alone, selected with the counts the bench line reports:
+python3 $R/tools/timed_stats.py $(find $out/stats_${variant}_${prec} -name "*kernel_trace.csv" -print -quit) \
+  $out/bench_under_rocprof_${variant}_${prec}.log $out/${variant}_${prec}_bench_kernel \
+  > $out/timed_stats_${variant}_${prec}.json || exit $?
+# counter calibration at the kernels' access widths (FETCH_SIZE and WRITE_SIZE passes of a known byte count)
+if [ "${CALIB:-1}" == 1 ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 120 rocprofv3 --pmc $c --kernel-trace -d $out/calib_$c -o calib --output-format csv \
+      -- python3 $R/tools/calib_counters.py run > $out/calib_$c.log 2>&1 || exit $?
+  done
+  python3 $R/tools/calib_counters.py analyse $out/calib_FETCH_SIZE $out/calib_WRITE_SIZE $R/profiles/traffic_latest.json \
+    > $out/calib.json || exit $?
+fi
 cp $R/profiles/traffic_latest.json $out/traffic_latest.json
