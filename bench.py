@@ -59,6 +59,9 @@ def parse():
                         "by default and reports as pcie_inclusive -- the reference GPU drivers' TOTAL semantics "
                         "(cloudsc_driver.cu:344-456), never the headline value")
     p.add_argument("--transfer-steps", type=int, default=7)
+    p.add_argument("--no-boundary", action="store_true",
+                   help="skip the caller-owned-buffer leg (cloudsc_fields_alloc + cloudsc_gpu_run) that N=1 runs "
+                        "and reports as boundary_path")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="host threads of the CPU baseline (default: OMP_NUM_THREADS, else all host cores)")
     p.add_argument("--no-hbm-peak", action="store_true", help="skip the in-run STREAM-copy measurement")
@@ -222,6 +225,65 @@ def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
                     "cloudsc_driver.cu:344,456), host-buffer path over PCIe; NOT the headline value"}
 
 
+def boundary_path(ca, g, ds, args, prec, variant, np, launches=30):
+    """The reference CUDA driver's shape on caller-owned buffers: every field
+    allocated by cloudsc_fields_alloc (one buffer per field, the outputs placed
+    by the write-pattern search), the inputs copied in (from the state's buffers,
+    device to device), the KSEG kernel launched through cloudsc_gpu_run on them,
+    plude restored before each launch, HIP events on the null stream around each
+    launch.  Reports the median kernel time and the search's cost beside the
+    state's: what a caller of the low-level boundary gets."""
+    import ctypes as C
+    lib = ca.gpu_lib()
+    hip = C.CDLL("libamdhip64.so")
+    for fn, at in (("hipMalloc", [C.POINTER(C.c_void_p), C.c_size_t]), ("hipFree", [C.c_void_p]),
+                   ("hipMemset", [C.c_void_p, C.c_int, C.c_size_t]), ("hipEventCreate", [C.POINTER(C.c_void_p)]),
+                   ("hipEventRecord", [C.c_void_p, C.c_void_p]), ("hipEventSynchronize", [C.c_void_p]),
+                   ("hipEventDestroy", [C.c_void_p]),
+                   ("hipEventElapsedTime", [C.POINTER(C.c_float), C.c_void_p, C.c_void_p])):
+        getattr(hip, fn).argtypes = at
+    sf = ca.Fields()
+    ca.check(lib.cloudsc_state_fields(g.h, C.byref(sf)))
+    p = ca.Params.from_dict(ds.params)
+    ca.check(lib.cloudsc_gpu_init(0, C.byref(p)))
+    df = ca.DeviceFields(args.ngptot, args.nproma, ds.klev, prec)
+    ws, e0, e1 = C.c_void_p(), C.c_void_p(), C.c_void_p()
+    try:
+        df.copy_from(sf, list(ca.INPUT_FIELDS))
+        nb = lib.cloudsc_gpu_scratch_bytes(prec, variant, args.ngptot, args.nproma, ds.klev)
+        assert hip.hipMalloc(C.byref(ws), nb) == 0 and hip.hipMemset(ws, 0, 256) == 0
+        hip.hipEventCreate(C.byref(e0))
+        hip.hipEventCreate(C.byref(e1))
+        ms = []
+        for i in range(launches + 5):
+            ca.check(lib.cloudsc_state_reset(g.h))   # the state's plude buffer <- its pristine input
+            ca.check(lib.cloudsc_state_sync(g.h))
+            df.copy_from(sf, ["plude"])
+            hip.hipEventRecord(e0, None)
+            ca.check(lib.cloudsc_gpu_run(0, None, prec, variant, args.ngptot, args.nproma, ds.klev, C.byref(df.f),
+                                         ws))
+            hip.hipEventRecord(e1, None)
+            hip.hipEventSynchronize(e1)
+            t = C.c_float()
+            hip.hipEventElapsedTime(C.byref(t), e0, e1)
+            if i >= 5:
+                ms.append(t.value)
+        ca.check(lib.cloudsc_gpu_check(0, None, variant, ws))
+    finally:
+        for e in (e0, e1):
+            if e.value:
+                hip.hipEventDestroy(e)
+        if ws.value:
+            hip.hipFree(ws)
+        rep = df.report.to_dict()
+        df.close()
+    return {"kernel_ms_median": round(float(np.median(ms)), 4), "kernel_ms_min": round(float(np.min(ms)), 4),
+            "launches": len(ms), "placement": rep,
+            "method": "cloudsc_fields_alloc (outputs placed by the write-pattern search) + cloudsc_gpu_run, the "
+                      "reference CUDA driver's allocate / copy in / launch shape (cloudsc_driver.cu:276-416); "
+                      "HIP events on the null stream around each launch (the KSEG prepare kernel included)"}
+
+
 def energy_window(g, variant, cp, pw_file, seconds, ncols, np):
     """Board power while the kernel runs back to back for `seconds` (after the
     timed region, untimed): mean W over the window and the energy per column =
@@ -325,6 +387,9 @@ def main():
     worst = 0.0
     for (mn, mx, maxerr, errsum, refsum) in (st[:5] for st in stats):
         worst = max(worst, errsum / refsum if refsum > 0 else errsum)
+    boundary = None
+    if not args.no_boundary and world == 1 and kind == ca.VARIANT_KSEG:
+        boundary = boundary_path(ca, g, ds, args, prec, variant, np)
     g.close()
 
     if rank != 0:
@@ -402,6 +467,8 @@ def main():
         line["roofline"]["frac_of_achievable"] = round(achieved / peak_meas, 4)
     if not args.no_transfer and world == 1:
         line["pcie_inclusive"] = transfer_rate(ca, ds, args, prec, variant)
+    if boundary is not None:
+        line["boundary_path"] = boundary
     if not args.no_cpu_baseline and world == 1:
         nth = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(ca, ds, nth)
