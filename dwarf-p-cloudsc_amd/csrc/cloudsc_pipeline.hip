@@ -453,8 +453,17 @@ int run_on_engines(cloudsc_host_pipeline* p, int variant, int vk, double* ms) {
     // plude: after the slot's previous D2H has read it back (with one slot
     // that D2H is the previous chunk's, not issued yet)
     if (reuse) {
-      if (out_issued < c - nslots && (rc = drain(c - nslots))) break;
-      if ((rc = wait(p->sig_out[c % nslots]))) break;
+      if (out_issued < c - nslots) rc = drain(c - nslots);
+      if (!rc) rc = wait(p->sig_out[c % nslots]);
+      if (rc) {
+        // part 1 is never issued: take its copies off the count part 0 set,
+        // or the final wait below would never see the signal reach zero
+        int n1 = 0;
+        for (int i = 0; i < kNumFields; i++)
+          if (hf[i] && kFieldTable[i].dir == FD_INOUT) n1++;
+        hsa_signal_subtract_screlease(p->sig_in[c % nslots], n1);
+        break;
+      }
     }
     if ((rc = issue(c, true, 1))) break;
     // the previous chunk's outputs, as soon as its kernel is done
