@@ -55,18 +55,36 @@ CLOUDSC_HD T ldg(const T* ubase, size_t uidx, unsigned lane_bytes) {
   return *(const T*)((const char*)(ubase + uidx) + lane_bytes);
 }
 // Outputs are written once and never read back by the kernel, and the level
-// inputs are read once: both go as non-temporal (streaming) accesses, so the
-// caches keep what is re-read (the neighbour levels, the hand-off state).
-// -1.9 % kernel time on the same box (profiles/r01/ab_nontemporal.txt).
+// inputs are read once: the inputs are non-temporal (streaming) loads, so the
+// caches keep what is re-read (the neighbour levels, the hand-off state)
+// (-1.9 % kernel time with nt loads and stores, profiles/r01/ab_nontemporal.txt).
+// The outputs are write-through stores (sc1: an agent-scope relaxed atomic store
+// lowers to global_store ... sc1, which leaves no line of it in the XCD's L2;
+// plain and nt stores keep theirs, MI355X_MICROARCH.md): -0.7...-0.8 % fp64 and
+// -0.5 % fp32 against nt stores, the same bits (profiles/r05/experiments_kernel_ab.txt).
 // stg_cached is for scratch that is read back (the SCC variant's temporaries).
 template <typename T>
 CLOUDSC_HD void stg_cached(T* ubase, size_t uidx, unsigned lane_bytes,
                                            typename std::common_type<T>::type v) {
   *(T*)((char*)(ubase + uidx) + lane_bytes) = v;
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// the write-through store of one output element (4 or 8 bytes, naturally aligned)
+template <typename T, typename P>
+__device__ __forceinline__ void st_wt(P* p, T v) {
+  using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned>::type;
+  U bits;
+  __builtin_memcpy(&bits, &v, sizeof(T));
+  __hip_atomic_store((U*)p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
 template <typename T>
 CLOUDSC_HD void stg(T* ubase, size_t uidx, unsigned lane_bytes, typename std::common_type<T>::type v) {
-  __builtin_nontemporal_store(v, (T*)((char*)(ubase + uidx) + lane_bytes));
+#if defined(__HIP_DEVICE_COMPILE__)
+  st_wt<T>((char*)(ubase + uidx) + lane_bytes, (T)v);
+#else
+  *(T*)((char*)(ubase + uidx) + lane_bytes) = v;
+#endif
 }
 // a level input, read exactly once
 template <typename T>
@@ -95,8 +113,7 @@ CLOUDSC_HD void stg_u(T* ubase, size_t uidx, unsigned lane_bytes, typename std::
 #if defined(__HIP_DEVICE_COMPILE__)
   T* p = ubase + uidx;
   asm("" : "+s"(p));
-  using GT = __attribute__((address_space(1))) T;
-  __builtin_nontemporal_store(v, (GT*)((__attribute__((address_space(1))) char*)p + lane_bytes));
+  st_wt<T>((__attribute__((address_space(1))) char*)p + lane_bytes, (T)v);
 #else
   stg(ubase, uidx, lane_bytes, v);
 #endif
