@@ -287,27 +287,29 @@ def boundary_path(ca, g, ds, args, prec, variant, np, launches=30):
 def energy_window(g, variant, cp, pw_file, seconds, ncols, np):
     """Board power while the kernel runs back to back for `seconds` (after the
     timed region, untimed): mean W over the window and the energy per column =
-    mean W x mean kernel time / columns.  The sensor averages over ~1-10 ms,
+    mean W x time per launch / columns.  The sensor averages over ~1-10 ms,
     longer than one 1.6 ms launch, so the window is long; the timed region's
     own mean W is reported beside it."""
     if not pw_file:
         return {"board_w": None, "energy_uj_per_column": None, "source": "no hwmon power file for this device"}
     s = cp.PowerSampler(pw_file)
     s.start()
-    t0, ms = time.perf_counter(), []
+    t0, span, n = time.perf_counter(), 0.0, 0
     while time.perf_counter() - t0 < seconds:
-        ms.extend(g.run(variant, 50).tolist())
+        span += g.run_span(variant, 50)
+        n += 50
     g.sync()
     s.stop()
     w = s.mean_w()
-    k = float(np.mean(ms))
+    k = span / n
     return {"board_w": round(w, 1) if w else None,
             "energy_uj_per_column": round(w * k * 1e-3 / ncols * 1e6, 3) if w else None,
-            "kernel_ms": round(k, 4), "launches": len(ms), "samples": len(s.samples),
+            "kernel_ms": round(k, 4), "launches": n, "samples": len(s.samples),
             "seconds": round(time.perf_counter() - t0, 2), "source": pw_file,
             "method": "hwmon board power sampled every 10 ms while the kernel ran back to back after the timed "
-                      "region; energy per column = mean W x mean kernel time / columns (the reference reads "
-                      "energy beside its timings: EC_PMON, src/common/module/ec_pmon_mod.F90)"}
+                      "region (plain launches, timed 50 at a time); energy per column = mean W x time per launch / "
+                      "columns (the reference reads energy beside its timings: EC_PMON, "
+                      "src/common/module/ec_pmon_mod.F90)"}
 
 
 def main():
@@ -355,14 +357,18 @@ def main():
     ctl.barrier()
     sampler.start()
     t0 = time.perf_counter()
-    kernel_ms = g.run(variant, args.steps)      # one launch per step; its dispatch records its events
+    # one plain launch per step, the K launches bracketed by two events on the state's stream: a dispatch
+    # that records its own events leaves ~5 us more between kernels (profiles/r05/launch_forms.txt)
+    span_ms = g.run_span(variant, args.steps)
     g.sync()
     t1 = time.perf_counter()
     sampler.stop()
     ctl.barrier()
     wall = ctl.max(t1 - t0)
-    k_avg_ms = ctl.max(float(np.mean(kernel_ms)))
+    k_avg_ms = ctl.max(span_ms / args.steps)
     sclk = g.kseg_clock() if kind == ca.VARIANT_KSEG else None
+    # the launch-time distribution: the same K launches again, each recording its own events (untimed)
+    kernel_ms = g.run(variant, args.steps)
     energy = energy_window(g, variant, cp, pw_file, args.energy_seconds, ncols, np) if args.energy_seconds > 0 \
         else None
     if energy is not None:
@@ -372,7 +378,7 @@ def main():
     # timing table, src/common/module/timer_mod.F90:160-167)
     mine = {"rank": rank, "device": device, "local_rank": topo.local_rank, "ngptot": ncols,
             "col_offset": col_offset, "wall_s": round(t1 - t0, 6),
-            "kernel_ms": round(float(np.mean(kernel_ms)), 4), "kernel_ms_min": round(float(np.min(kernel_ms)), 4),
+            "kernel_ms": round(span_ms / args.steps, 4), "kernel_ms_min": round(float(np.min(kernel_ms)), 4),
             "kernel_ms_median": round(float(np.median(kernel_ms)), 4),
             "stream_gbs": round(peak_meas, 1) if peak_meas else None,
             "sclk_ghz": round(sclk, 4) if sclk else None, "prewarm_steps": prewarm,
@@ -435,8 +441,10 @@ def main():
         "kernel_ms_median": round(float(np.median(kernel_ms)), 4),
         "kernel_ms_p10": round(float(np.percentile(kernel_ms, 10)), 4),
         "kernel_ms_p90": round(float(np.percentile(kernel_ms, 90)), 4),
-        "kernel_ms_method": "HIP events recorded by each launch's own dispatch on the state's stream; mean over "
-                            "ranks' means is the max over ranks",
+        "kernel_ms_method": "the timed region's K launches between two HIP events on the state's stream, / K (the "
+                            "~1 us dispatch boundaries included); max over ranks.  min/median/p10/p90: a second "
+                            "pass of K launches after the timed region, each recording its own events (+5 us "
+                            "between kernels, not in the timed region)",
         "sclk_ghz": round(sclk, 4) if sclk else None,
         "sclk_method": "effective shader clock of the timed launches: each workgroup's s_memtime cycles over its "
                        "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",

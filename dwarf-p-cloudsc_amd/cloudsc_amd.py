@@ -404,6 +404,7 @@ def gpu_lib(path: Optional[str] = None):
     lib.cloudsc_state_create.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_longlong, C.POINTER(Template), C.POINTER(Params)]
     lib.cloudsc_state_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]
+    lib.cloudsc_state_run_span.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]
     lib.cloudsc_state_validate.argtypes = [C.c_void_p, C.POINTER(Reference), C.POINTER(Stats)]
     lib.cloudsc_state_download.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
     lib.cloudsc_state_field_elems.argtypes = [C.c_void_p, C.c_int]
@@ -597,6 +598,13 @@ class GpuState:
         ms = (C.c_float * reps)()
         check(self.lib.cloudsc_state_run(self.h, variant, reps, ms))
         return np.array(ms[:], dtype=np.float64)
+
+    def run_span(self, variant: int = VARIANT_KCACHE, reps: int = 1) -> float:
+        """`reps` plain launches timed as a whole (cloudsc_state_run_span): ms from
+        the first launch's start to the last one's end."""
+        ms = C.c_float()
+        check(self.lib.cloudsc_state_run_span(self.h, variant, reps, C.byref(ms)))
+        return float(ms.value)
 
     def sync(self) -> None:
         check(self.lib.cloudsc_state_sync(self.h))

@@ -651,7 +651,74 @@ int cloudsc_state_reset(cloudsc_gpu_state_t* s) {
   return CLOUDSC_OK;
 }
 
-int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) {
+#if defined(CLOUDSC_DEBUG_KNOBS) || defined(CLOUDSC_DEBUG_LAUNCH_FORMS)
+// Diagnostic (debug builds only): the time between consecutive physics launches.
+// `reps` launches back to back, timed as a whole by two stream events; mode 0 =
+// the product form (each dispatch records its own event pair), 1 = plain
+// dispatches, 2 = one hipGraph holding the workspace reset and the `reps`
+// launches (KSEG's epoch arguments are baked into the graph, so the graph
+// starts from a zeroed workspace), replayed once for warm-up and once timed.
+int cloudsc_debug_launch_forms(cloudsc_gpu_state_t* s, int variant, int reps, int mode, double* ms) {
+  if (!s || reps <= 0 || mode < 0 || mode > 2 || !ms) return CLOUDSC_EINVAL;
+  int rc = cloudsc_state_run(s, variant, 1, nullptr);   // workspace allocated and warm
+  if (rc) return rc;
+  void* scratch = variant_kind(variant) == CLOUDSC_VARIANT_SCC ? s->scratch
+                  : variant_kind(variant) == CLOUDSC_VARIANT_KSEG ? s->kseg_ws : nullptr;
+  hipEvent_t t0, t1;
+  HIPCHK(hipEventCreate(&t0));
+  HIPCHK(hipEventCreate(&t1));
+  std::vector<hipEvent_t> ev(2 * (size_t)reps);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  auto issue = [&](bool events) {
+    int r0 = CLOUDSC_OK;
+    for (int r = 0; r < reps && r0 == CLOUDSC_OK; r++) {
+      const LaunchEvents lev{ev[2 * r], ev[2 * r + 1]};
+      r0 = gpu_run_impl(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f, scratch,
+                        s->plude_pristine, &s->params, &s->kseg_epoch, events ? &lev : nullptr);
+    }
+    return r0;
+  };
+  float t = 0.f;
+  if (mode < 2) {
+    HIPCHK(hipEventRecord(t0, s->stream));
+    rc = issue(mode == 0);
+    HIPCHK(hipEventRecord(t1, s->stream));
+  } else {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    s->kseg_epoch.ready = false;   // the graph's first launch zeroes the workspace
+    HIPCHK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+    rc = issue(false);
+    HIPCHK(hipStreamEndCapture(s->stream, &g));
+    if (rc == CLOUDSC_OK) HIPCHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    if (rc == CLOUDSC_OK) HIPCHK(hipGraphLaunch(ge, s->stream));
+    HIPCHK(hipEventRecord(t0, s->stream));
+    if (rc == CLOUDSC_OK) HIPCHK(hipGraphLaunch(ge, s->stream));
+    HIPCHK(hipEventRecord(t1, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    if (ge) (void)hipGraphExecDestroy(ge);
+    if (g) (void)hipGraphDestroy(g);
+    s->kseg_epoch.ready = false;   // the device counters no longer match the host's epoch
+  }
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipEventElapsedTime(&t, t0, t1));
+  *ms = t / reps;
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(t0);
+  (void)hipEventDestroy(t1);
+  if (rc == CLOUDSC_OK && variant_kind(variant) == CLOUDSC_VARIANT_KSEG)
+    rc = kseg_check(s->device, s->stream, scratch);
+  return rc;
+}
+#endif
+
+// The launches of cloudsc_state_run (per_launch: each dispatch records its own
+// event pair, ms[r]; ms may be NULL, then plain dispatches) and of
+// cloudsc_state_run_span (plain dispatches bracketed by two stream events,
+// *span_ms).  A dispatch that records events costs ~5 us more between kernels
+// than a plain one (fp64 6.2 against 1.3 us above the kernel's duration,
+// fp32 5.3 against 0.7 us; profiles/r05/launch_forms.txt).
+static int state_launches(cloudsc_gpu_state_t* s, int variant, int reps, float* ms, float* span_ms) {
   if (!s || reps <= 0) return CLOUDSC_EINVAL;
   HIPCHK(hipSetDevice(s->device));
   void* scratch = nullptr;
@@ -667,26 +734,40 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
     }
     scratch = ws;
   }
-  std::vector<hipEvent_t> ev(2 * (size_t)reps);
-  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  // per-launch pairs, or the two bracketing events of a span
+  std::vector<hipEvent_t> ev(ms ? 2 * (size_t)reps : span_ms ? 2 : 0);
   int rc = CLOUDSC_OK;
+  for (auto& e : ev) {
+    hipError_t ce = hipEventCreate(&e);
+    if (ce != hipSuccess) { e = nullptr; rc = hip_fail(ce, "hipEventCreate"); }
+  }
+  if (rc == CLOUDSC_OK && span_ms) {
+    hipError_t re = hipEventRecord(ev[0], s->stream);
+    if (re != hipSuccess) rc = hip_fail(re, "hipEventRecord");
+  }
   for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
     // out of place: every step reads the pristine plude and writes the INOUT
     // result to f.plude, so repeated steps see the same input with no restore copy
-    // the physics kernel's dispatch records the pair itself: no event packets between steps
-    const LaunchEvents lev{ev[2 * r], ev[2 * r + 1]};
+    const LaunchEvents lev{ms ? ev[2 * r] : nullptr, ms ? ev[2 * r + 1] : nullptr};
     rc = gpu_run_impl(s->device, s->stream, s->precision, variant, s->ngptot, s->nproma, s->klev, &s->f, scratch,
-                      s->plude_pristine, &s->params, &s->kseg_epoch, &lev);
+                      s->plude_pristine, &s->params, &s->kseg_epoch, ms ? &lev : nullptr);
+  }
+  if (rc == CLOUDSC_OK && span_ms) {
+    hipError_t re = hipEventRecord(ev[1], s->stream);
+    if (re != hipSuccess) rc = hip_fail(re, "hipEventRecord");
   }
   hipError_t e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess && rc == CLOUDSC_OK) rc = hip_fail(e, "hipStreamSynchronize");
-  for (int r = 0; r < reps && rc == CLOUDSC_OK; r++) {
-    float t = 0.f;
-    e = hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]);
+  for (int r = 0; ms && r < reps && rc == CLOUDSC_OK; r++) {
+    e = hipEventElapsedTime(&ms[r], ev[2 * r], ev[2 * r + 1]);
     if (e != hipSuccess) rc = hip_fail(e, "hipEventElapsedTime");
-    if (ms) ms[r] = t;
   }
-  for (auto& x : ev) (void)hipEventDestroy(x);
+  if (span_ms && rc == CLOUDSC_OK) {
+    e = hipEventElapsedTime(span_ms, ev[0], ev[1]);
+    if (e != hipSuccess) rc = hip_fail(e, "hipEventElapsedTime");
+  }
+  for (auto& x : ev)
+    if (x) (void)hipEventDestroy(x);
   if (rc == CLOUDSC_OK && vk == CLOUDSC_VARIANT_KSEG) {
     // a segment whose predecessor never arrived gives up after a bounded spin
     // and counts itself in the workspace's error word: its results are
@@ -697,6 +778,15 @@ int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) 
   }
   if (rc != CLOUDSC_OK) s->kseg_epoch.ready = false;   // zero the workspace again before the next launch
   return rc;
+}
+
+int cloudsc_state_run(cloudsc_gpu_state_t* s, int variant, int reps, float* ms) {
+  return state_launches(s, variant, reps, ms, nullptr);
+}
+
+int cloudsc_state_run_span(cloudsc_gpu_state_t* s, int variant, int reps, float* span_ms) {
+  if (!span_ms) return CLOUDSC_EINVAL;
+  return state_launches(s, variant, reps, nullptr, span_ms);
 }
 
 int cloudsc_state_kseg_clock(cloudsc_gpu_state_t* s, int reset, double* ghz) {

@@ -473,9 +473,17 @@ int cloudsc_state_reset(cloudsc_gpu_state_t *state);
  * is taken out of place: every step reads the pristine input copy and writes
  * its result to the state's plude buffer, so repeated steps compute the same
  * step without a restore copy.  ms_per_step[reps] receives the per-step
- * kernel time (may be NULL).  KSEG: CLOUDSC_EHANDOFF if a segment hand-off
+ * kernel time, recorded by each launch's own dispatch (may be NULL: then no
+ * events are recorded).  KSEG: CLOUDSC_EHANDOFF if a segment hand-off
  * timed out (cloudsc_gpu_check). */
 int cloudsc_state_run(cloudsc_gpu_state_t *state, int variant, int reps, float *ms_per_step);
+
+/* As cloudsc_state_run, timed as a whole: `reps` plain dispatches back to
+ * back between two events on the state's stream; *span_ms = the time from the
+ * first launch's start to the last one's end.  A dispatch that records its own
+ * events (cloudsc_state_run with ms_per_step) leaves ~5 us more between
+ * kernels than a plain one; span_ms / reps is the sustained time per step. */
+int cloudsc_state_run_span(cloudsc_gpu_state_t *state, int variant, int reps, float *span_ms);
 
 /* Wait for all work of the state's stream. */
 int cloudsc_state_sync(cloudsc_gpu_state_t *state);

@@ -255,6 +255,39 @@ def test_kseg_consecutive_launches_on_one_workspace(lib, ds, nproma):
         g.close()
 
 
+@pytest.mark.parametrize("precision", [ca.FP64, ca.FP32])
+def test_run_span_plain_launches(lib, ds, precision):
+    """cloudsc_state_run_span (bench.py's timed region): plain dispatches timed
+    as a whole give the same bits as the per-launch-event form, on a fresh
+    workspace and continuing one; the span covers the launches (at least the
+    sum of the shortest single launches, at most a few ms more than their
+    per-launch sum); invalid arguments are refused; a hand-off timeout is
+    reported the same way."""
+    g = ca.GpuState(ds, 20000, 64, precision)
+    try:
+        span = g.run_span(ca.VARIANT_KSEG, 5)            # first call: zeroes the workspace
+        first = g.outputs()
+        per = g.run(ca.VARIANT_KSEG, 5)
+        assert bitwise_mismatches(g.outputs(), first) == {}
+        assert 5 * per.min() * 0.5 <= span <= per.sum() + 5.0, (span, per)
+        assert g.run_span(ca.VARIANT_KSEG, 3) > 0
+        assert bitwise_mismatches(g.outputs(), first) == {}
+        assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KCACHE), first) == {}
+        ms = C.c_float()
+        assert lib.cloudsc_state_run_span(g.h, ca.VARIANT_KSEG, 0, C.byref(ms)) == ca.EINVAL
+        assert lib.cloudsc_state_run_span(g.h, ca.VARIANT_KSEG, 2, None) == ca.EINVAL
+        ca.kseg_spin_limit(0)
+        try:
+            with pytest.raises(ca.CloudscError):
+                g.run_span(ca.VARIANT_KSEG, 2)
+        finally:
+            ca.kseg_spin_limit(-1)
+        g.run_span(ca.VARIANT_KSEG, 2)
+        assert bitwise_mismatches(g.outputs(), first) == {}
+    finally:
+        g.close()
+
+
 def test_kseg_more_blocks_than_grid_y_limit(lib, ds):
     """KSEG at 163840 columns with NPROMA 2: 81,920 blocks, more than HIP's
     65,536 limit on a grid's y/z dimension.  The expansion and validation
