@@ -637,6 +637,33 @@ int cloudsc_debug_state_relocate_field(cloudsc_gpu_state_t* s, int member) {
   return CLOUDSC_OK;
 }
 
+// Diagnostic: move one of the state's buffers that are not fields to fresh
+// memory (the old one stays with the state until it is destroyed): which = 0
+// the pristine plude copy, 1 the KSEG workspace (zeroed again before the next
+// launch), 2 the SCC temporaries.
+int cloudsc_debug_state_relocate_aux(cloudsc_gpu_state_t* s, int which) {
+  if (!s || which < 0 || which > 2) return CLOUDSC_EINVAL;
+  void** slot = which == 0 ? &s->plude_pristine : which == 1 ? &s->kseg_ws : &s->scratch;
+  if (!*slot) return CLOUDSC_EINVAL;
+  const size_t bytes =
+      which == 0 ? field_elems(s, 0) * s->es
+                 : (size_t)cloudsc_gpu_scratch_bytes(s->precision, which == 1 ? CLOUDSC_VARIANT_KSEG : CLOUDSC_VARIANT_SCC,
+                                                     s->ngptot, s->nproma, s->klev);
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  void* q = nullptr;
+  int rc = dalloc(s, &q, bytes);
+  if (rc) return rc;
+  if (which == 0) HIPCHK(hipMemcpyAsync(q, *slot, bytes, hipMemcpyDeviceToDevice, s->stream));
+  if (which == 1) {
+    HIPCHK(hipMemsetAsync(q, 0, 256, s->stream));
+    s->kseg_epoch.ready = false;
+  }
+  HIPCHK(hipStreamSynchronize(s->stream));
+  *slot = q;
+  return CLOUDSC_OK;
+}
+
 int cloudsc_state_fields(const cloudsc_gpu_state_t* s, cloudsc_fields_t* out) {
   if (!s || !out) return CLOUDSC_EINVAL;
   *out = s->f;

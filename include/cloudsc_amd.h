@@ -463,6 +463,12 @@ int cloudsc_debug_kernel_copy(void *dst, const void *src, long long bytes);
  * hold (aerosol fields it was created without). */
 int cloudsc_debug_state_relocate_field(cloudsc_gpu_state_t *s, int member);
 
+/* Diagnostic: the same for a state buffer that is not a field: which = 0 the
+ * pristine plude copy, 1 the KSEG workspace (zeroed again before the next
+ * launch), 2 the SCC temporaries.  CLOUDSC_EINVAL when the state does not hold
+ * it yet (workspaces are allocated on first use). */
+int cloudsc_debug_state_relocate_aux(cloudsc_gpu_state_t *s, int which);
+
 /* Restore plude from the pristine copy -- for callers that run in place
  * through cloudsc_gpu_run on the state's buffers. */
 int cloudsc_state_reset(cloudsc_gpu_state_t *state);
