@@ -20,7 +20,9 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--states", type=int, default=16)
     p.add_argument("--nproma", type=int, nargs="+", default=[64, 128, 256])
+    p.add_argument("--passes", type=int, default=-1, help="field passes of the search (-1: the library's default)")
     a = p.parse_args()
+    ca.check(ca.gpu_lib().cloudsc_set_placement_search(a.passes))
     ds = ca.load_dataset()
     states, times = [], []
     try:
@@ -37,8 +39,8 @@ def main():
                                      r["launches"], r["search_ms"], r["peak_transient_bytes"] / 1e9), flush=True)
         lo = min(times)
         slow = [i for i, t in enumerate(times) if t > 1.07 * lo]
-        print("lib %s: %d states, fastest %.4f, median %.4f, slowest %.4f, > 1.07x fastest: %d %s"
-              % (os.path.basename(os.environ.get("CLOUDSC_AMD_LIB", ca.LIB_PATH)), len(times), lo,
+        print("lib %s passes %d: %d states, fastest %.4f, median %.4f, slowest %.4f, > 1.07x fastest: %d %s"
+              % (os.path.basename(os.environ.get("CLOUDSC_AMD_LIB", ca.LIB_PATH)), a.passes, len(times), lo,
                  stt.median(times), max(times), len(slow), slow), flush=True)
     finally:
         for g in states:
