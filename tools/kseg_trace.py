@@ -23,8 +23,8 @@ prec = ca.FP64 if (len(sys.argv) < 2 or sys.argv[1] == "fp64") else ca.FP32
 ngptot, nproma = 163840, int(os.environ.get("TRACE_NPROMA", "64"))
 nb = (ngptot // nproma) * ((nproma + 63) // 64)   # one-wave items: 64-column sub-blocks
 g = ca.GpuState(ds, ngptot, nproma, prec)
-for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,3,4").split(",")]:
-    os.environ["CLOUDSC_KSEG_NSEG"] = str(nseg)
+for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "2,1,3").split(",")]:
+    ca.kseg_schedule(nseg, 0)      # segments per column (0 = the default)
     g.run(ca.VARIANT_KSEG, 2)
     ms = g.run(ca.VARIANT_KSEG, 1)
     n = nseg * nb
@@ -67,4 +67,5 @@ for nseg in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,3,4").spl
     out["dur_us_by_start_bin"] = [round(float(dur[sbin == i].mean()), 1) if np.any(sbin == i) else None
                                   for i in range(20)]
     print(json.dumps(out), flush=True)
+ca.kseg_schedule(0, 0)
 g.close()
