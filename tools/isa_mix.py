@@ -8,7 +8,7 @@ the VALU share and where the register moves come from (VGPR copies, SGPR
 materialisations, constants).  Static counts: code inside branches counts
 once whether or not a wave takes it.
 
-usage: isa_mix.py fp64|fp32"""
+usage: isa_mix.py fp64|fp32 [extra hipcc flags...]"""
 import collections
 import os
 import re
@@ -27,7 +27,7 @@ def main():
                            "-mllvm", "-disable-machine-licm", "-I" + os.path.join(REPO, "include"),
                            "-I" + os.path.join(REPO, "dwarf-p-cloudsc_amd", "csrc"), "-DCLOUDSC_ONLY_KSEG=%d" % es,
                            "--cuda-device-only", "-S", os.path.join(REPO, "dwarf-p-cloudsc_amd", "csrc", "cloudsc_gpu.hip"),
-                           "-o", out], stderr=subprocess.DEVNULL)
+                           "-o", out] + sys.argv[2:], stderr=subprocess.DEVNULL)
     L = open(out).read().split("\n")
     # the product kernel: no aerosols, no LDS carry; fp32 FAST (last flag 1), fp64 exact (0)
     name = r"^_Z10kseg_entryI%sLi2ELi%dELb0ELb0ELb%dE.*:" % ("d" if es == 8 else "f", 3 if es == 8 else 1,
