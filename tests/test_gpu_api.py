@@ -348,6 +348,32 @@ def test_state_field_placement_is_transparent(lib, ds):
         assert diff == {}, (precision, diff)
 
 
+def test_state_buffer_relocation_is_transparent(lib, ds):
+    """The slow-state diagnostics (tools/slow_state_diag.py) move a live state's
+    workspace, pristine plude copy and fields to fresh memory: the next KSEG run
+    zeroes the moved workspace and every output stays bit-equal.  A buffer the
+    state does not hold yet (the SCC temporaries before an SCC run) and unknown
+    selectors are refused."""
+    lib.cloudsc_debug_state_relocate_aux.argtypes = [C.c_void_p, C.c_int]
+    lib.cloudsc_debug_state_relocate_field.argtypes = [C.c_void_p, C.c_int]
+    names = [f[0] for f in ca.Fields._fields_]
+    g = ca.GpuState(ds, 5000, 64)
+    try:
+        ref = outputs_of(g, ca.VARIANT_KSEG, reps=2)
+        assert lib.cloudsc_debug_state_relocate_aux(g.h, 2) == ca.EINVAL      # no SCC scratch yet
+        assert lib.cloudsc_debug_state_relocate_aux(g.h, 3) == ca.EINVAL
+        assert lib.cloudsc_debug_state_relocate_aux(None, 0) == ca.EINVAL
+        for which in (1, 0):                                                  # workspace, pristine plude
+            ca.check(lib.cloudsc_debug_state_relocate_aux(g.h, which))
+            assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=2), ref) == {}, which
+        for name in ("pt", "paph", "tendency_loc_cld", "pfplsn", "plude"):
+            ca.check(lib.cloudsc_debug_state_relocate_field(g.h, names.index(name)))
+        assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KSEG, reps=2), ref) == {}
+        assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KCACHE), ref) == {}
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("precision", [ca.FP64, ca.FP32])
 def test_output_placement_search(lib, ds, precision):
     """The output placement search at state creation (cloudsc_state_placement)
