@@ -14,9 +14,11 @@ kernel launch reading every input (plude from the state's pristine copy: the
 INOUT field is taken out of place, so repeated steps are the same step) and
 writing every output.  The timed region brackets exactly K steps with barrier
 + device sync on both sides; value = all columns of all ranks / max-over-ranks
-wall time.  The kernel alone is also timed with HIP start/stop events on the
-launch stream, recorded by the kernel's own dispatch packet
-(hipExtLaunchKernelGGL; roofline.achieved uses that kernel time).
+wall time.  The K launches are plain dispatches, timed as a whole by two HIP
+events on the launch stream (cloudsc_state_run_span): roofline.achieved uses
+that time / K.  A second, untimed pass of K launches, each recording its own
+start/stop events in its dispatch packet (hipExtLaunchKernelGGL), gives the
+per-launch distribution (kernel_ms_median / p10 / p90).
 """
 import argparse
 import json
