@@ -273,6 +273,9 @@ def test_run_span_plain_launches(lib, ds, precision):
         assert g.run_span(ca.VARIANT_KSEG, 3) > 0
         assert bitwise_mismatches(g.outputs(), first) == {}
         assert bitwise_mismatches(outputs_of(g, ca.VARIANT_KCACHE), first) == {}
+        for v in (ca.VARIANT_KCACHE, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE):   # the other kernels, span-timed
+            assert g.run_span(v, 2) > 0
+            assert bitwise_mismatches(g.outputs(), first) == {}, v
         ms = C.c_float()
         assert lib.cloudsc_state_run_span(g.h, ca.VARIANT_KSEG, 0, C.byref(ms)) == ca.EINVAL
         assert lib.cloudsc_state_run_span(g.h, ca.VARIANT_KSEG, 2, None) == ca.EINVAL
