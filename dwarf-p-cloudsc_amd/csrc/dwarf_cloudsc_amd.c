@@ -39,6 +39,8 @@
 #include <float.h>
 #include <limits.h>
 #include <math.h>
+#include <dirent.h>
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -56,6 +58,7 @@ typedef struct {
   int numomp, ngptot, nproma, ngpus, precision, variant, reps, warmup;
   int transfer, chunk_blocks, nstreams, exact_libm;
   int place;                      /* placement search: 1 on, 0 off, -1 auto (on when reps > 1) */
+  double energy_s;                /* --energy: seconds of back-to-back launches sampled for board power */
   double tol;
   int tol_given;
   const char *input_h5, *reference_h5, *data_dir, *write_h5_dir;
@@ -64,6 +67,7 @@ typedef struct {
 typedef struct {
   int device, ngptot, nproma, precision, variant, reps, warmup;
   int libm_bit;                   /* CLOUDSC_FP32_EXACT_LIBM or 0 */
+  double energy_s;
   long long col_offset;
   const cloudsc_template_t *tmpl;
   const cloudsc_params_t *params;
@@ -75,6 +79,9 @@ typedef struct {
   double t_start, t_end;          /* seconds, CLOCK_MONOTONIC */
   float *kernel_ms;
   cloudsc_placement_t place;      /* the state's placement search and its cost */
+  char power_path[512];           /* the device's hwmon power file ("" = none) */
+  double board_w, energy_ms_per_step;   /* mean board power over the energy window, and its time per launch */
+  int power_samples, energy_steps;
   cloudsc_stats_t stats[CLOUDSC_NVALID];
 } shard_t;
 
@@ -107,6 +114,9 @@ static void usage(const char *prog) {
           "  --place on|off|auto   output placement search at state creation (~0.5 s, ~250 kernel\n"
           "                        launches; default auto: on when --reps > 1, off for one step)\n"
           "  --warmup W            untimed steps before the timed ones (default 1)\n"
+          "  --energy S            after the timed steps, S seconds of back-to-back launches with the\n"
+          "                        device's board power sampled every 10 ms (hwmon power1_input):\n"
+          "                        prints an ENERGY line per shard (uJ per column)\n"
           "  --input FILE          input HDF5 file (default ./input.h5 when present)\n"
           "  --reference FILE      reference HDF5 file (default ./reference.h5 when present)\n"
           "  --data DIR            raw dataset directory (default $CLOUDSC_DATA or the\n"
@@ -149,6 +159,12 @@ static int parse(int argc, char **argv, options_t *o) {
       else { fprintf(stderr, "bad variant %s\n", v); return -1; }
     } else if (!strcmp(a, "--reps")) { NEEDV(); o->reps = atoi(v); }
     else if (!strcmp(a, "--warmup")) { NEEDV(); o->warmup = atoi(v); }
+    else if (!strcmp(a, "--energy")) {
+      NEEDV();
+      char *end;
+      o->energy_s = strtod(v, &end);
+      if (*end || !(o->energy_s >= 0.0) || o->energy_s > 600.0) { fprintf(stderr, "bad --energy %s\n", v); return -1; }
+    }
     else if (!strcmp(a, "--place")) {
       NEEDV();
       if (!strcmp(v, "on")) o->place = 1;
@@ -210,6 +226,91 @@ static void default_data_dir(char *out, size_t n) {
 
 static int exists(const char *p) { return access(p, R_OK) == 0; }
 
+/* ---- board power (--energy): the reference reads energy beside its timings
+ * (EC_PMON, src/common/module/ec_pmon_mod.F90, dwarf_cloudsc.F90:42-46).  On an
+ * MI355X host the GPU's sensor is its hwmon power file in microwatts, found
+ * through the device's PCI bus id (hipDeviceGetPCIBusId, from the HIP runtime
+ * the library has loaded); read-only. ---- */
+static void power_file(int device, char *out, size_t n) {
+  out[0] = 0;
+  void *hip = dlopen("libamdhip64.so", RTLD_NOW | RTLD_NOLOAD);
+  if (!hip) hip = dlopen("libamdhip64.so", RTLD_NOW);
+  if (!hip) return;
+  int (*bus_id)(char *, int, int) = (int (*)(char *, int, int))dlsym(hip, "hipDeviceGetPCIBusId");
+  char bus[64];
+  if (!bus_id || bus_id(bus, (int)sizeof(bus), device) != 0) return;
+  for (char *c = bus; *c; c++)
+    if (*c >= 'A' && *c <= 'F') *c = (char)(*c - 'A' + 'a');
+  char dir[256];
+  snprintf(dir, sizeof(dir), "/sys/bus/pci/devices/%s/hwmon", bus);
+  DIR *d = opendir(dir);
+  if (!d) return;
+  struct dirent *e;
+  while ((e = readdir(d))) {
+    if (strncmp(e->d_name, "hwmon", 5)) continue;
+    static const char *names[2] = {"power1_input", "power1_average"};
+    for (int k = 0; k < 2 && !out[0]; k++) {
+      char f[512];
+      snprintf(f, sizeof(f), "%.256s/%.64s/%.32s", dir, e->d_name, names[k]);
+      FILE *fp = fopen(f, "r");
+      if (!fp) continue;
+      long long uw;
+      if (fscanf(fp, "%lld", &uw) == 1) snprintf(out, n, "%s", f);
+      fclose(fp);
+    }
+    if (out[0]) break;
+  }
+  closedir(d);
+}
+
+typedef struct {
+  const char *path;
+  volatile int stop;
+  double sum_w;
+  int n;
+} sampler_t;
+
+static void *sampler_main(void *arg) {
+  sampler_t *sp = (sampler_t *)arg;
+  const struct timespec period = {0, 10 * 1000 * 1000};
+  while (!sp->stop) {
+    FILE *fp = fopen(sp->path, "r");
+    if (fp) {
+      long long uw;
+      if (fscanf(fp, "%lld", &uw) == 1) { sp->sum_w += uw * 1e-6; sp->n++; }
+      fclose(fp);
+    }
+    nanosleep(&period, NULL);
+  }
+  return NULL;
+}
+
+/* S seconds of back-to-back launches (plain dispatches, timed 20 at a time) with
+ * the board power sampled: mean W and the time per launch, for the ENERGY line */
+static int energy_window(shard_t *s, cloudsc_gpu_state_t *st) {
+  power_file(s->device, s->power_path, sizeof(s->power_path));
+  if (!s->power_path[0]) return CLOUDSC_OK;
+  sampler_t sp = {s->power_path, 0, 0.0, 0};
+  pthread_t th;
+  if (pthread_create(&th, NULL, sampler_main, &sp)) return CLOUDSC_OK;
+  const double t0 = now();
+  double span_ms = 0.0;
+  int steps = 0, rc = CLOUDSC_OK;
+  while (!rc && now() - t0 < s->energy_s) {
+    float ms = 0.f;
+    rc = cloudsc_state_run_span(st, s->variant | s->libm_bit, 20, &ms);
+    span_ms += ms;
+    steps += 20;
+  }
+  sp.stop = 1;
+  pthread_join(th, NULL);
+  s->power_samples = sp.n;
+  s->board_w = sp.n ? sp.sum_w / sp.n : 0.0;
+  s->energy_steps = steps;
+  s->energy_ms_per_step = steps ? span_ms / steps : 0.0;
+  return rc;
+}
+
 static void *shard_main(void *arg) {
   shard_t *s = (shard_t *)arg;
   cloudsc_gpu_state_t *st = NULL;
@@ -229,6 +330,9 @@ static void *shard_main(void *arg) {
   if (!s->rc) s->rc = cloudsc_state_sync(st);
   s->t_end = now();
   pthread_barrier_wait(s->barrier);
+  /* untimed; every launch is the same step (plude is taken out of place), so
+   * the validation below still checks the timed step's results */
+  if (!s->rc && s->energy_s > 0.0) s->rc = energy_window(s, st);
   if (!s->rc && s->ref) s->rc = cloudsc_state_validate(st, s->ref, s->stats);
   if (s->rc) snprintf(s->err, sizeof(s->err), "%s", cloudsc_last_hip_error());
   if (st) cloudsc_state_destroy(st);
@@ -438,6 +542,7 @@ int main(int argc, char **argv) {
     }
     printf(" CLOUDSC-AMD: fp64, variant cpu (cloudsc_cpu_run, %d host thread(s)); state: %s\n", o.numomp,
            ds.source);
+    if (o.energy_s > 0.0) printf(" ENERGY: n/a (host variant: no GPU board power)\n");
     rc = run_host(&o, &ds);
     cloudsc_io_free(&ds);
     return rc;
@@ -457,6 +562,7 @@ int main(int argc, char **argv) {
            o.precision == CLOUDSC_FP64 ? "fp64" : "fp32",
            variant_name(o.variant),
            ds.source);
+    if (o.energy_s > 0.0) printf(" ENERGY: n/a (the host-buffer path is bound by PCIe; run without --transfer)\n");
     rc = run_host(&o, &ds);
     cloudsc_io_free(&ds);
     return rc;
@@ -495,6 +601,7 @@ int main(int argc, char **argv) {
     s->device = d % ndev; s->ngptot = (int)cols; s->col_offset = col; s->nproma = o.nproma;
     s->precision = o.precision; s->variant = o.variant; s->reps = o.reps; s->warmup = o.warmup;
     s->libm_bit = o.exact_libm ? CLOUDSC_FP32_EXACT_LIBM : 0;
+    s->energy_s = o.energy_s;
     s->tmpl = &tmpl; s->params = &ds.params; s->ref = ds.has_reference ? &ref : NULL; s->barrier = &bar;
     s->kernel_ms = (float *)calloc((size_t)o.reps, sizeof(float));
     col += cols;
@@ -563,6 +670,17 @@ int main(int argc, char **argv) {
     printf(" PLACEMENT: shard=%d search=kernel first_ms=%.4f kept_ms=%.4f tries=%d moves=%d launches=%d "
            "search_ms=%.1f peak_transient_MB=%.1f\n", d, pl->probe_first_ms, pl->probe_final_ms, pl->tries,
            pl->moves, pl->launches, pl->search_ms, pl->peak_transient_bytes / 1048576.0);
+  }
+  /* board power over the energy window (--energy): uJ per column = W x ms per launch / columns */
+  for (int d = 0; d < nused && o.energy_s > 0.0; d++) {
+    if (!sh[d].power_path[0] || !sh[d].power_samples) {
+      printf(" ENERGY: shard=%d device=%d n/a (no hwmon power file for this device)\n", d, sh[d].device);
+      continue;
+    }
+    printf(" ENERGY: shard=%d device=%d board_w=%.1f samples=%d steps=%d ms_per_step=%.4f uj_per_column=%.3f "
+           "source=%s\n", d, sh[d].device, sh[d].board_w, sh[d].power_samples, sh[d].energy_steps,
+           sh[d].energy_ms_per_step, sh[d].board_w * sh[d].energy_ms_per_step * 1e3 / sh[d].ngptot,
+           sh[d].power_path);
   }
 
   /* ---- validation (cloudsc_validate.c:193-216, combined over devices) ---- */

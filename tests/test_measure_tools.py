@@ -132,3 +132,18 @@ def test_cli_place_option():
     ok = subprocess.run([dwarf, "1", "200", "16", "--variant", "cpu", "--place", "off"], capture_output=True,
                         text=True, timeout=120)
     assert ok.returncode == 0 and "VALIDATION: PASSED" in ok.stdout, ok.stdout[-1500:] + ok.stderr
+
+
+def test_cli_energy_option():
+    dwarf = os.path.join(REPO, "dwarf-p-cloudsc_amd", "dwarf-cloudsc-amd")
+    if not os.path.exists(dwarf):
+        pytest.skip("dwarf-cloudsc-amd not built")
+    for v in ("-1", "x", "1000"):
+        bad = subprocess.run([dwarf, "1", "100", "4", "--energy", v], capture_output=True, text=True)
+        assert bad.returncode != 0 and "bad --energy" in bad.stderr
+    usage = subprocess.run([dwarf, "--help"], capture_output=True, text=True)
+    assert "--energy S" in usage.stderr
+    ok = subprocess.run([dwarf, "1", "200", "16", "--variant", "cpu", "--energy", "0.1"], capture_output=True,
+                        text=True, timeout=120)
+    assert ok.returncode == 0 and "VALIDATION: PASSED" in ok.stdout, ok.stdout[-1500:] + ok.stderr
+    assert " ENERGY: n/a (host variant" in ok.stdout
