@@ -119,9 +119,16 @@ int launch_kseg_cfg("""),
         if (hipHostMalloc((void**)&pinned, bytes, hipHostMallocDefault) != hipSuccess) return CLOUDSC_ENOMEM;
         pcap = bytes;
       }
-      std::memcpy(pinned, tab.data(), bytes);
       unsigned* dtab = (unsigned*)((char*)pa.state + ((size_t)pa.nblocks * kCarryN * nproma * sizeof(real) + 255) / 256 * 256);
-      HIPCHK(hipMemcpyAsync(dtab, pinned, bytes, hipMemcpyHostToDevice, st));
+      static thread_local const void* last_dtab = nullptr;
+      static thread_local std::vector<unsigned> last_tab;
+      if (dtab != last_dtab || tab != last_tab) {       // upload once per workspace and schedule
+        std::memcpy(pinned, tab.data(), bytes);
+        HIPCHK(hipMemcpyAsync(dtab, pinned, bytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        last_dtab = dtab;
+        last_tab = tab;
+      }
       pg.wtab = dtab;
       pg.wstride = wstride;
       for (int q = 0; q < kKsegStripes; q++) pg.witems[q] = witems[q];
