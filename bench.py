@@ -33,6 +33,7 @@ BYTES_PER_COL = {8: 56036, 4: 28020}     # SURVEY.md §8d algorithmic bytes per 
 # of which read (inputs incl. plude and ktype): 3701 values + 4 B; written: 3303 values
 IN_BYTES_PER_COL = {8: 3701 * 8 + 4, 4: 3701 * 4 + 4}
 HBM_PEAK_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GUIDE_COPY_GBS = 6290.0                  # MI355X_MICROARCH.md:36, measured float4 copy (79 % of the spec)
 
 
 def parse():
@@ -129,6 +130,7 @@ def cpu_baseline(ca, ds, nthreads):
     full = [r for r in runs if r["cmd"].split()[1] == "163840"]
     best = max(full, key=lambda r: r["columns_per_s"])
     return {"value": best["columns_per_s"], "unit": "columns/s", "cores": nthreads, "kind": kind,
+            "host": dict(host_cores(), threads_used=nthreads),
             "sample": "%s `%s` (163840 columns, the full workload; the faster NPROMA of 16/32), OpenMP block "
                       "loop timed like cloudsc_driver.c:181-231, validated vs reference.h5" % (
                           "reference kernel src/cloudsc_c/cloudsc/cloudsc_c.c compiled from its sources"
@@ -136,6 +138,50 @@ def cpu_baseline(ca, ds, nthreads):
             "runs": runs,
             "cpu_variant": {"what": "this library's cloudsc_cpu_run (the GPU kernels' phase functions "
                                     "compiled for the host), same states", "runs": product}}
+
+
+def launch_histogram(ms, np, width_us=10.0):
+    """Counts of the per-launch times in `width_us` bins: {"lo_ms", "width_us", "counts"}."""
+    a = np.asarray(ms, dtype=np.float64)
+    lo = np.floor(a.min() * 1e3 / width_us) * width_us / 1e3
+    idx = np.floor((a - lo) * 1e3 / width_us + 1e-9).astype(int)
+    return {"lo_ms": round(float(lo), 4), "width_us": width_us,
+            "counts": [int(c) for c in np.bincount(idx)]}
+
+
+def host_cores():
+    """The host CPU share the CPU baseline ran on: nproc (every CPU the machine
+    has), the CPUs this process may run on (sched_getaffinity), the sockets and
+    the model (from /sys and /proc/cpuinfo; best effort).  On the GPU pool the
+    box's share is 16 threads (OMP_NUM_THREADS) of a much larger machine."""
+    out = {"nproc": os.cpu_count(), "affinity_cpus": None, "sockets": None, "model": None,
+           "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+        out["affinity_cpus"] = len(aff)
+        pk = set()
+        for c in aff:
+            try:
+                pk.add(open("/sys/devices/system/cpu/cpu%d/topology/physical_package_id" % c).read().strip())
+            except OSError:
+                pass
+        out["affinity_sockets"] = len(pk) or None
+        allpk = set()
+        for d in os.listdir("/sys/devices/system/cpu"):
+            f = "/sys/devices/system/cpu/%s/topology/physical_package_id" % d
+            if d.startswith("cpu") and d[3:].isdigit() and os.path.exists(f):
+                allpk.add(open(f).read().strip())
+        out["sockets"] = len(allpk) or None
+    except (OSError, AttributeError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                out["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return out
 
 
 def roofline_traffic(ca, path, key):
@@ -369,13 +415,22 @@ def main():
     wall = ctl.max(t1 - t0)
     k_avg_ms = ctl.max(span_ms / args.steps)
     sclk = g.kseg_clock() if kind == ca.VARIANT_KSEG else None
-    # the launch-time distribution: the same K launches again, each recording its own events (untimed)
+    # the launch-time distribution: the same K launches again, each recording its own events (untimed),
+    # with that pass's own effective shader clock (so a slow tail of launches shows whether the clock moved)
+    if kind == ca.VARIANT_KSEG:
+        g.kseg_clock(reset=True)
     kernel_ms = g.run(variant, args.steps)
+    sclk2 = g.kseg_clock() if kind == ca.VARIANT_KSEG else None
     energy = energy_window(g, variant, cp, pw_file, args.energy_seconds, ncols, np) if args.energy_seconds > 0 \
         else None
     if energy is not None:
-        energy["timed_region_board_w"] = round(sampler.mean_w(), 1) if sampler.mean_w() else None
-        energy["timed_region_samples"] = len(sampler.samples)
+        # the timed region's own board power only from >= 20 samples (4 samples of a sensor
+        # that averages over 1-10 ms meant nothing); 100 launches of 1.65 ms give ~17 at 10 ms
+        n_tr = len(sampler.samples)
+        energy["timed_region_samples"] = n_tr
+        energy["timed_region_board_w"] = round(sampler.mean_w(), 1) if sampler.mean_w() and n_tr >= 20 else None
+        if n_tr < 20:
+            energy["timed_region_board_w_note"] = "not reported: %d samples < 20 (see board_w over the window)" % n_tr
     # every rank's own record, gathered to rank 0 (the reference's per-rank
     # timing table, src/common/module/timer_mod.F90:160-167)
     mine = {"rank": rank, "device": device, "local_rank": topo.local_rank, "ngptot": ncols,
@@ -447,6 +502,11 @@ def main():
                             "~1 us dispatch boundaries included); max over ranks.  min/median/p10/p90: a second "
                             "pass of K launches after the timed region, each recording its own events (+5 us "
                             "between kernels, not in the timed region)",
+        "second_pass": {"sclk_ghz": round(sclk2, 4) if sclk2 else None,
+                        "kernel_ms_hist": launch_histogram(kernel_ms, np),
+                        "kernel_ms_all": [round(float(x), 4) for x in kernel_ms],
+                        "method": "the per-launch times behind kernel_ms_median/p10/p90 (order of launch) and that "
+                                  "pass's own effective shader clock (cloudsc_state_kseg_clock reset before it)"},
         "sclk_ghz": round(sclk, 4) if sclk else None,
         "sclk_method": "effective shader clock of the timed launches: each workgroup's s_memtime cycles over its "
                        "s_memrealtime ticks, summed in the KSEG workspace (cloudsc_state_kseg_clock)",
@@ -472,9 +532,14 @@ def main():
     if peak_meas:
         line["roofline"]["achievable_peak"] = {
             "value": round(peak_meas, 1), "unit": "GB/s",
-            "method": "STREAM copy on this device in this run (cloudsc_hbm_copy_gbps: 2 x 4 GiB, the best of "
-                      "cached and non-temporal grid-stride / tile copies, 10 launches each)"}
+            "method": "STREAM copy on this device in this run (cloudsc_hbm_copy_gbps: three pairs of 2 GiB "
+                      "buffers, 8 / 16 / 64 KiB tiles per workgroup, non-temporal and cached, 10 launches of each "
+                      "shape per pair, the best launch)"}
         line["roofline"]["frac_of_achievable"] = round(achieved / peak_meas, 4)
+    # the same against MI355X_MICROARCH.md's measured float4 copy (a fixed figure, not this box's)
+    line["roofline"]["guide_copy_peak"] = {"value": GUIDE_COPY_GBS, "unit": "GB/s",
+                                           "source": "MI355X_MICROARCH.md:36 (float4 copy, measured)"}
+    line["roofline"]["frac_of_guide_copy"] = round(achieved / GUIDE_COPY_GBS, 4)
     if not args.no_transfer and world == 1:
         line["pcie_inclusive"] = transfer_rate(ca, ds, args, prec, variant)
     if boundary is not None:

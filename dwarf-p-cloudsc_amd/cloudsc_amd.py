@@ -130,13 +130,14 @@ class Placement(C.Structure):
     """cloudsc_placement_t: what a placement search cost and found."""
     _fields_ = [("probe_first_ms", C.c_float), ("probe_final_ms", C.c_float), ("tries", C.c_int),
                 ("moves", C.c_int), ("launches", C.c_int), ("method", C.c_int), ("search_ms", C.c_double),
-                ("peak_transient_bytes", C.c_longlong)]
+                ("peak_transient_bytes", C.c_longlong), ("transient_budget_bytes", C.c_longlong)]
 
     def to_dict(self) -> dict:
         return {"probe_first_ms": round(self.probe_first_ms, 4), "probe_final_ms": round(self.probe_final_ms, 4),
                 "tries": self.tries, "moves": self.moves, "launches": self.launches,
                 "method": {0: "none", 1: "kernel", 2: "write-probe"}.get(self.method, self.method),
-                "search_ms": round(self.search_ms, 1), "peak_transient_bytes": self.peak_transient_bytes}
+                "search_ms": round(self.search_ms, 1), "peak_transient_bytes": self.peak_transient_bytes,
+                "transient_budget_bytes": self.transient_budget_bytes}
 
 
 PLACE_NONE = 1

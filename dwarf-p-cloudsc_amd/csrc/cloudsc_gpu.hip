@@ -253,7 +253,8 @@ template <> struct DefaultCfg<float> {
 #define CLOUDSC_FOR_EACH_CFG(X) \
   X(10, 1, 0, false) X(11, 1, 1, false) X(20, 2, 0, false) X(21, 2, 1, false) X(30, 3, 0, false) \
   X(31, 3, 1, false) X(40, 4, 0, false) X(41, 4, 1, false) X(120, 2, 0, true) X(121, 2, 1, true) X(23, 2, 3, false) X(24, 2, 4, false) X(33, 3, 3, false) \
-  X(122, 2, 2, true) X(130, 3, 0, true) X(132, 3, 2, true) X(22, 2, 2, false) X(131, 3, 1, true) X(140, 4, 0, true)
+  X(122, 2, 2, true) X(130, 3, 0, true) X(132, 3, 2, true) X(22, 2, 2, false) X(131, 3, 1, true) X(140, 4, 0, true) \
+  X(123, 2, 3, true) X(133, 3, 3, true)
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;

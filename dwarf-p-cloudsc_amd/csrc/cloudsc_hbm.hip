@@ -4,11 +4,19 @@
 // pool's boxes differ by 10+ % in this kernel, so the spec fraction alone does
 // not normalise).
 //
-// A STREAM copy b[i] = a[i] over two device buffers, 16 B per lane per access
-// and four independent loads in flight per lane before the stores, in a few
-// shapes (cached or non-temporal; a resident grid striding over the buffer, or
-// one 16 KB tile per workgroup); the figure is the best launch of any shape.
-// Bytes moved = 2 x buffer size per launch.
+// A STREAM copy b[i] = a[i] over two device buffers, 16 B per lane per access,
+// one tile per workgroup (each lane's loads of its tile in flight before its
+// stores), cached or non-temporal; the figure is the best launch of any shape
+// over three buffer pairs.  Bytes moved = 2 x buffer size per launch.
+//
+// Round 6 (the in-run figure read 5.9-6.27 TB/s where
+// MI355X_MICROARCH.md quotes 6.29 TB/s): a sweep of shapes and buffer pairs
+// (tools/stream_sweep.hip, profiles/r06/stream_sweep.jsonl) found the 16 KiB
+// non-temporal tile the fastest shape by far (6.18-6.48 TB/s over three pairs
+// on one box; persistent grid-stride forms with 2-16 loads in flight per lane
+// at 16-64 waves per CU: 4.7-5.2 TB/s; 32 / 64 KiB tiles 4.4 / 5.6 TB/s), and
+// the buffers' placement moving it by 5 %: so three pairs are measured (held
+// together, so each gets pages of its own) and the best launch counts.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,78 +43,73 @@ __device__ __forceinline__ void st(u32x4* p, u32x4 v) {
   else *p = v;
 }
 
-// persistent grid-stride form: four independent 16-B loads per lane in flight
-template <bool NT>
-__global__ void __launch_bounds__(256) copy_strided(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const u32x4 v0 = ld<NT>(a + i), v1 = ld<NT>(a + i + stride), v2 = ld<NT>(a + i + 2 * stride),
-                v3 = ld<NT>(a + i + 3 * stride);
-    st<NT>(b + i, v0); st<NT>(b + i + stride, v1); st<NT>(b + i + 2 * stride, v2); st<NT>(b + i + 3 * stride, v3);
-  }
-  for (; i < n; i += stride) st<NT>(b + i, ld<NT>(a + i));
-}
-
-// one-shot form: each lane copies 4 consecutive 16-B chunks of its workgroup's 16 KB tile
-template <bool NT>
+// one workgroup per tile of 256 x U 16-B vectors: lane t copies t, t + 256, ...
+template <int U, bool NT>
 __global__ void __launch_bounds__(256) copy_tiles(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n) {
-  const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
-  u32x4 v[4];
+  const size_t base = (size_t)blockIdx.x * (256 * U) + threadIdx.x;
+  u32x4 v[U];
 #pragma unroll
-  for (int q = 0; q < 4; q++)
+  for (int q = 0; q < U; q++)
     if (base + q * 256 < n) v[q] = ld<NT>(a + base + q * 256);
 #pragma unroll
-  for (int q = 0; q < 4; q++)
+  for (int q = 0; q < U; q++)
     if (base + q * 256 < n) st<NT>(b + base + q * 256, v[q]);
 }
 
 }  // namespace
 
 extern "C" int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, double* gbps) {
-  if (!gbps || bytes < (1 << 20) || reps <= 0) return CLOUDSC_EINVAL;
+  if (!gbps || bytes < (2 << 20) || reps <= 0) return CLOUDSC_EINVAL;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CLOUDSC_ENODEV;
   HIPCHK(hipSetDevice(device));
-  const size_t nvec = (size_t)bytes / sizeof(u32x4);
-  void *a = nullptr, *b = nullptr;
-  if (hipMalloc(&a, nvec * sizeof(u32x4)) != hipSuccess) return CLOUDSC_ENOMEM;
-  if (hipMalloc(&b, nvec * sizeof(u32x4)) != hipSuccess) { (void)hipFree(a); return CLOUDSC_ENOMEM; }
-  int ncu = 256;
-  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-  // the shapes tried; the achievable figure is the best of them
-  struct Shape { void (*k)(const u32x4*, u32x4*, size_t); int grid; };
-  const int tiles = (int)((nvec + 1023) / 1024);
-  const Shape shapes[] = {{copy_strided<true>, ncu * 8},  {copy_strided<false>, ncu * 8},
-                          {copy_strided<true>, ncu * 16}, {copy_tiles<true>, tiles},
-                          {copy_tiles<false>, tiles}};
+  // three pairs of `bytes` / 2 each (the total footprint of one pair of `bytes`
+  // times 1.5); each buffer stays far beyond the 256 MiB Infinity Cache
+  constexpr int kPairs = 3;
+  const size_t nvec = (size_t)bytes / 2 / sizeof(u32x4);
+  void* buf[2 * kPairs] = {};
+  int rc = CLOUDSC_OK;
+  for (int i = 0; i < 2 * kPairs && rc == CLOUDSC_OK; i++)
+    if (hipMalloc(&buf[i], nvec * sizeof(u32x4)) != hipSuccess) { (void)hipGetLastError(); rc = CLOUDSC_ENOMEM; }
+  // the shapes tried; the achievable figure is the best launch of any of them
+  struct Shape { void (*k)(const u32x4*, u32x4*, size_t); int vecs; };
+  const Shape shapes[] = {{copy_tiles<4, true>, 1024}, {copy_tiles<2, true>, 512}, {copy_tiles<4, false>, 1024},
+                          {copy_tiles<16, true>, 4096}};
+  constexpr int ns = (int)(sizeof(shapes) / sizeof(shapes[0]));
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  int rc = CLOUDSC_OK;
   double best_ms = 0.0;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
-      hipEventCreate(&e1) != hipSuccess) {
-    rc = CLOUDSC_EHIP;
-  } else if (hipMemsetAsync(a, 0x3c, nvec * sizeof(u32x4), st) != hipSuccess) {
-    rc = CLOUDSC_EHIP;
-  } else {
-    for (int r = -1; r < reps * (int)(sizeof(shapes) / sizeof(shapes[0])) && rc == CLOUDSC_OK; r++) {
-      const Shape& sh = shapes[(r < 0 ? 0 : r) % (int)(sizeof(shapes) / sizeof(shapes[0]))];   // r = -1: warm-up
-      if (hipEventRecord(e0, st) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
-      hipLaunchKernelGGL(sh.k, dim3(sh.grid), dim3(256), 0, st, (const u32x4*)a, (u32x4*)b, nvec);
-      if (hipGetLastError() != hipSuccess || hipEventRecord(e1, st) != hipSuccess ||
-          hipEventSynchronize(e1) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
+  hipError_t e = hipSuccess;
+  if (rc == CLOUDSC_OK) {
+    e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    for (int i = 0; i < 2 * kPairs && e == hipSuccess; i += 2)
+      e = hipMemsetAsync(buf[i], 0x3c, nvec * sizeof(u32x4), st);
+  }
+  for (int pr = 0; pr < kPairs && rc == CLOUDSC_OK && e == hipSuccess; pr++) {
+    const u32x4* a = (const u32x4*)buf[2 * pr];
+    u32x4* b = (u32x4*)buf[2 * pr + 1];
+    for (int r = -1; r < reps * ns && e == hipSuccess; r++) {
+      const Shape& sh = shapes[(r < 0 ? 0 : r) % ns];   // r = -1: warm-up
+      e = hipEventRecord(e0, st);
+      if (e != hipSuccess) break;
+      hipLaunchKernelGGL(sh.k, dim3((unsigned)((nvec + sh.vecs - 1) / sh.vecs)), dim3(256), 0, st, a, b, nvec);
+      e = hipGetLastError();
+      if (e == hipSuccess) e = hipEventRecord(e1, st);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
       float ms = 0.f;
-      if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) { rc = CLOUDSC_EHIP; break; }
-      if (r >= 0 && (best_ms == 0.0 || ms < best_ms)) best_ms = ms;
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      if (e == hipSuccess && r >= 0 && (best_ms == 0.0 || ms < best_ms)) best_ms = ms;
     }
   }
+  if (rc == CLOUDSC_OK && e != hipSuccess) rc = hip_fail(e, "hbm copy measurement");
   if (rc == CLOUDSC_OK) *gbps = 2.0 * (double)(nvec * sizeof(u32x4)) / (best_ms * 1e-3) / 1e9;
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   if (st) (void)hipStreamDestroy(st);
-  (void)hipFree(a);
-  (void)hipFree(b);
+  for (void* p : buf)
+    if (p) (void)hipFree(p);
   return rc;
 }
 

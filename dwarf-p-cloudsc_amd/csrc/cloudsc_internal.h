@@ -107,9 +107,12 @@ int kseg_clock(int device, void* stream, void* scratch, bool reset, double* ghz,
 
 // the memory-pattern probe of cloudsc_place.hip over f on `stream`: best of
 // `reps` timed launches after one untimed, ms; mode 0 outputs written only, 1
-// inputs read too (every non-NULL output of f is overwritten)
+// inputs read too (every non-NULL output of f is overwritten); strides (6, may
+// be NULL): the inputs' and outputs' block / row / species element strides of
+// another layout (cloudsc_debug_memory_probe_layout)
 int memory_probe(int device, hipStream_t stream, int precision, int ngptot, int nproma, int klev,
-                 const cloudsc_fields_t* f, int mode, int reps, hipEvent_t e0, hipEvent_t e1, float* best_ms);
+                 const cloudsc_fields_t* f, int mode, int reps, hipEvent_t e0, hipEvent_t e1, float* best_ms,
+                 const long long* strides = nullptr);
 
 // What a placement search cost and found (cloudsc_place.hip)
 struct PlaceCost {
@@ -118,6 +121,7 @@ struct PlaceCost {
   int launches = 0;                       // probe launches (untimed ones included)
   double search_ms = 0.0;                 // wall time of the search
   long long peak_bytes = 0;               // most candidate and spacer bytes held at once
+  long long budget_bytes = 0;             // the bound search_fits was asked for (peak_bytes stays below it)
 };
 // the output placement search (see cloudsc_place.hip): moves f's output
 // members (members/bytes: positions in cloudsc_fields_t and sizes) to the
@@ -138,6 +142,9 @@ void dev_free(void* p);
 // fits the device's free memory with room to spare (on a device
 // shared by several ranks the search must not starve their allocations)
 bool search_fits(size_t transient);
+// the transient bytes a placement search holds at most over sets of set_bytes
+// in n buffers with `sets` whole sets tried: two candidate sets and the spacers
+size_t search_transient_bytes(size_t set_bytes, int n, int sets);
 
 // copy ceiling on the pipelines' engine pair (cloudsc_pipeline.hip)
 int pcie_engine_gbps(int device, size_t nb, int reps, double* h2d, double* d2h, double* both);

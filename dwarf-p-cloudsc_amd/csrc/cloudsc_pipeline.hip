@@ -652,8 +652,9 @@ int cloudsc_host_pipeline_run(cloudsc_host_pipeline_t* p, int variant, double* m
       if (hipMalloc(&q, (size_t)nb) != hipSuccess) return CLOUDSC_ENOMEM;
       p->allocs.push_back(q);
       // control words of a fresh KSEG workspace (recycled memory may hold a
-      // matching tag and a stale hand-off error count)
-      if (hipMemset(q, 0, 256) != hipSuccess) return CLOUDSC_EHIP;
+      // matching tag and a stale hand-off error count), zeroed on the stream
+      // that launches the kernels, so the order is the stream's
+      if (hipMemsetAsync(q, 0, 256, p->st_k) != hipSuccess) return CLOUDSC_EHIP;
       s.scratch = q;
       s.scratch_bytes = (size_t)nb;
     }

@@ -6,8 +6,8 @@
 // (DESIGN.md §3.12).  This file holds the measuring instrument that needs no
 // field contents: a memory-pattern probe that streams a field set the way the
 // KSEG kernel does -- one wave per 64-column sub-block, level by level, each
-// input plane read and each output plane written once, non-temporal -- with no
-// physics.  Its time on a set of device pointers ranks placements without the
+// input plane read once (non-temporal) and each output plane written once
+// (write-through, like the kernel) -- with no physics.  Its time on a set of device pointers ranks placements without the
 // caller's inputs (tools/place_corr.py measures how well it ranks them against
 // the physics kernel).
 #include <hip/hip_runtime.h>
@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstring>
 #include <functional>
+#include <type_traits>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -40,15 +41,28 @@ struct ProbeArgs {
   void* out_half[kProbeOutHalf];
   void* out_surf;                     // prainfrac_toprfz
   int ngptot, nproma, klev, nsub, nitems;
+  // element strides of the inputs [0..2] and the outputs [3..5]: between blocks,
+  // between rows (levels), between species planes; 0 = the reference block
+  // layout (per kind: klev / klev+1 / 5 klev rows of nproma per block).  The
+  // layout study of round 6 (tools/layout_corr.py) sets them for other layouts.
+  long long bs_in, rs_in, ss_in, bs_out, rs_out, ss_out;
 };
 
 template <typename real>
 __device__ __forceinline__ real ldnt(const void* p, size_t i) {
   return __builtin_nontemporal_load((const real*)p + i);
 }
+// an output store exactly as the kernel issues it since round 5: write-through
+// (an agent-scope relaxed atomic store, global_store ... sc1; cloudsc_kcache.h
+// st_wt).  Until round 6 the probe stored non-temporal, the kernel's policy
+// before that change (the instrument ranked a write policy the
+// kernel no longer used).
 template <typename real>
-__device__ __forceinline__ void stnt(void* p, size_t i, real v) {
-  __builtin_nontemporal_store(v, (real*)p + i);
+__device__ __forceinline__ void st_out(void* p, size_t i, real v) {
+  using U = typename std::conditional<sizeof(real) == 8, unsigned long long, unsigned>::type;
+  U bits;
+  __builtin_memcpy(&bits, &v, sizeof(real));
+  __hip_atomic_store((U*)p + i, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // one wave per item (64-column sub-block of an NPROMA block); a grid of at most
@@ -68,12 +82,21 @@ __global__ void __launch_bounds__(64) place_probe_kernel(const ProbeArgs a) {
     const long long col = b * a.nproma + jl;
     if (jl >= a.nproma || col >= a.ngptot) continue;
     const size_t np = (size_t)a.nproma, kl = (size_t)a.klev;
-    const size_t lvl0 = (size_t)b * kl * np + jl, half0 = (size_t)b * (kl + 1) * np + jl;
-    const size_t spc0 = (size_t)b * 5 * kl * np + jl;
+    // per class (inputs, outputs): block offsets of the level / half-level /
+    // species fields, row and species strides (the reference layout unless set)
+    const size_t ub = (size_t)b;
+    const size_t il0 = ub * (a.bs_in ? (size_t)a.bs_in : kl * np) + jl;
+    const size_t ih0 = ub * (a.bs_in ? (size_t)a.bs_in : (kl + 1) * np) + jl;
+    const size_t is0 = ub * (a.bs_in ? (size_t)a.bs_in : 5 * kl * np) + jl;
+    const size_t irs = a.rs_in ? (size_t)a.rs_in : np, iss = a.ss_in ? (size_t)a.ss_in : kl * np;
+    const size_t ol0 = ub * (a.bs_out ? (size_t)a.bs_out : kl * np) + jl;
+    const size_t oh0 = ub * (a.bs_out ? (size_t)a.bs_out : (kl + 1) * np) + jl;
+    const size_t os0 = ub * (a.bs_out ? (size_t)a.bs_out : 5 * kl * np) + jl;
+    const size_t ors = a.rs_out ? (size_t)a.rs_out : np, oss = a.ss_out ? (size_t)a.ss_out : kl * np;
     real acc = (real)0, nxt[NL];
     auto load = [&](int k) {
       if constexpr (READ) {
-        const size_t il = lvl0 + (size_t)k * np;
+        const size_t il = il0 + (size_t)k * irs;
 #pragma unroll
         for (int q = 0; q < kProbeInLevel; q++) nxt[q] = a.in_level[q] ? ldnt<real>(a.in_level[q], il) : (real)0;
 #pragma unroll
@@ -81,37 +104,37 @@ __global__ void __launch_bounds__(64) place_probe_kernel(const ProbeArgs a) {
 #pragma unroll
           for (int s = 0; s < 4; s++)
             nxt[kProbeInLevel + 4 * q + s] =
-                a.in_species[q] ? ldnt<real>(a.in_species[q], spc0 + ((size_t)s * kl + k) * np) : (real)0;
-        nxt[NL - 1] = a.paph ? ldnt<real>(a.paph, half0 + (size_t)(k + 1) * np) : (real)0;
+                a.in_species[q] ? ldnt<real>(a.in_species[q], is0 + (size_t)s * iss + (size_t)k * irs) : (real)0;
+        nxt[NL - 1] = a.paph ? ldnt<real>(a.paph, ih0 + (size_t)(k + 1) * irs) : (real)0;
       }
     };
     load(0);
     const real v0 = (real)b;
 #pragma unroll
     for (int q = 0; q < kProbeOutHalf; q++)
-      if (a.out_half[q]) stnt<real>(a.out_half[q], half0, v0);
+      if (a.out_half[q]) st_out<real>(a.out_half[q], oh0, v0);
     for (int k = 0; k < a.klev; k++) {
       real cur[NL];
 #pragma unroll
       for (int q = 0; q < NL; q++) cur[q] = nxt[q];
       if (k + 1 < a.klev) load(k + 1);
-      const size_t il = lvl0 + (size_t)k * np;
+      const size_t ol = ol0 + (size_t)k * ors;
       const real v = v0 + (real)k;
 #pragma unroll
       for (int q = 0; q < kProbeOutLevel; q++)
-        if (a.out_level[q]) stnt<real>(a.out_level[q], il, v);
+        if (a.out_level[q]) st_out<real>(a.out_level[q], ol, v);
       if (a.out_species)
 #pragma unroll
-        for (int s = 0; s < 5; s++) stnt<real>(a.out_species, spc0 + ((size_t)s * kl + k) * np, v);
+        for (int s = 0; s < 5; s++) st_out<real>(a.out_species, os0 + (size_t)s * oss + (size_t)k * ors, v);
 #pragma unroll
       for (int q = 0; q < kProbeOutHalf; q++)
-        if (a.out_half[q]) stnt<real>(a.out_half[q], half0 + (size_t)(k + 1) * np, v);
+        if (a.out_half[q]) st_out<real>(a.out_half[q], oh0 + (size_t)(k + 1) * ors, v);
       if constexpr (READ) {
 #pragma unroll
         for (int q = 0; q < NL; q++) acc += cur[q];
       }
     }
-    if (a.out_surf) stnt<real>(a.out_surf, (size_t)b * np + jl, acc);
+    if (a.out_surf) st_out<real>(a.out_surf, (size_t)b * np + jl, acc);
   }
 }
 
@@ -151,8 +174,13 @@ namespace cloudsc_impl {
 // one untimed launch, in ms; mode 0 writes the outputs only, 1 also reads the
 // inputs.  Every non-NULL output of f is overwritten.
 int memory_probe(int device, hipStream_t stream, int precision, int ngptot, int nproma, int klev,
-                 const cloudsc_fields_t* f, int mode, int reps, hipEvent_t e0, hipEvent_t e1, float* best_ms) {
-  const ProbeArgs a = probe_args(f, ngptot, nproma, klev, mode == 1);
+                 const cloudsc_fields_t* f, int mode, int reps, hipEvent_t e0, hipEvent_t e1, float* best_ms,
+                 const long long* strides) {
+  ProbeArgs a = probe_args(f, ngptot, nproma, klev, mode == 1);
+  if (strides) {
+    a.bs_in = strides[0]; a.rs_in = strides[1]; a.ss_in = strides[2];
+    a.bs_out = strides[3]; a.rs_out = strides[4]; a.ss_out = strides[5];
+  }
   const dim3 grid((unsigned)std::min(a.nitems, 2048));
   float best = -1.f;
   for (int r = 0; r <= reps; r++) {
@@ -235,6 +263,15 @@ void dev_free(void* p) {
 }
 #endif
 
+// Transient bytes of a search over sets of set_bytes in n buffers, `sets`
+// whole sets tried: two candidate sets (the best so far and the one being
+// probed) and the spacers (<= 32 MiB before each buffer of every shuffled set,
+// held to the end of the set phase), the bound search_outputs and place_inputs
+// keep.
+size_t search_transient_bytes(size_t set_bytes, int n, int sets) {
+  return 2 * set_bytes + (size_t)(sets > 1 ? sets - 1 : 0) * ((size_t)n << 25);
+}
+
 bool search_fits(size_t transient) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) { (void)hipGetLastError(); return false; }
@@ -251,9 +288,14 @@ bool search_fits(size_t transient) {
 // when the probe is > 1 % faster.  The caller's original buffers are never
 // freed here: on return f holds the chosen pointers and the caller adopts the
 // new ones (and frees the originals they replaced) or reverts.  Every other
-// candidate is freed before return; rejected buffers are held until then, so
-// no retry gets the same pages back.  An allocation failure ends the phase
-// with the best placement so far.
+// candidate is freed before return.  Transient memory stays within two output
+// sets plus the spacers (search_transient_bytes, which the callers check with
+// search_fits): a losing whole set is freed at once, and the single-field
+// buffers a pass rejects or replaces are held to the end of that pass only (so
+// no retry within the pass gets the same pages back; the next set or pass is
+// kept off a freed loser's pages by the spacers and by its own fresh
+// allocations -- a repeat on a loser's pages is one wasted try, not an error).
+// An allocation failure ends the phase with the best placement so far.
 int search_outputs(cloudsc_fields_t& f, const int* members, const size_t* bytes, int n, int sets, int passes,
                    uint32_t seed, const std::function<float(const cloudsc_fields_t&)>& probe, PlaceCost& cost) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -337,6 +379,11 @@ int search_outputs(cloudsc_fields_t& f, const int* members, const size_t* bytes,
         held.push_back({p, bytes[q]});
       }
     }
+    // the pass's rejected and replaced buffers go now: at most one set of them
+    // exists at a time (holding every pass's until the end made the
+    // peak (1 + passes) sets, beyond what search_fits had checked for)
+    for (auto& h : held) drop(h.first, h.second);
+    held.clear();
     if (!moved) break;
   }
   for (auto& h : held) drop(h.first, h.second);
@@ -347,8 +394,33 @@ int search_outputs(cloudsc_fields_t& f, const int* members, const size_t* bytes,
 
 }  // namespace cloudsc_impl
 
+namespace cloudsc_impl {
+int memory_probe_strided(int device, int precision, int ngptot, int nproma, int klev, const cloudsc_fields_t* f,
+                         int mode, int reps, const long long* strides, float* ms);
+}
+
 extern "C" int cloudsc_debug_memory_probe(int device, int precision, int ngptot, int nproma, int klev,
                                           const cloudsc_fields_t* f, int mode, int reps, float* ms) {
+  return memory_probe_strided(device, precision, ngptot, nproma, klev, f, mode, reps, nullptr, ms);
+}
+
+// The probe over fields in another layout (round 6 layout study): strides[6] =
+// {block, row, species} element strides of the inputs, then of the outputs (0 =
+// the reference layout's); field pointers address row 0 of block 0 of each
+// field (species 0 of a species field).  The caller guarantees that every
+// addressed element lies inside its own allocation.
+extern "C" int cloudsc_debug_memory_probe_layout(int device, int precision, int ngptot, int nproma, int klev,
+                                                 const cloudsc_fields_t* f, int mode, int reps,
+                                                 const long long* strides, float* ms) {
+  if (!strides) return CLOUDSC_EINVAL;
+  for (int i = 0; i < 6; i++)
+    if (strides[i] < 0) return CLOUDSC_EINVAL;
+  return memory_probe_strided(device, precision, ngptot, nproma, klev, f, mode, reps, strides, ms);
+}
+
+int cloudsc_impl::memory_probe_strided(int device, int precision, int ngptot, int nproma, int klev,
+                                       const cloudsc_fields_t* f, int mode, int reps, const long long* strides,
+                                       float* ms) {
   if (!f || !ms || reps <= 0 || (mode != 0 && mode != 1)) return CLOUDSC_EINVAL;
   int rc = validate_run_args(device, precision, CLOUDSC_VARIANT_KSEG, ngptot, nproma, klev);
   if (rc) return rc;
@@ -356,8 +428,10 @@ extern "C" int cloudsc_debug_memory_probe(int device, int precision, int ngptot,
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) rc = CLOUDSC_EHIP;
-  if (!rc) rc = memory_probe(device, st, precision, ngptot, nproma, klev, f, mode, reps, e0, e1, ms);
+  hipError_t ce = hipEventCreate(&e0);
+  if (ce == hipSuccess) ce = hipEventCreate(&e1);
+  if (ce != hipSuccess) rc = hip_fail(ce, "hipEventCreate");
+  if (!rc) rc = memory_probe(device, st, precision, ngptot, nproma, klev, f, mode, reps, e0, e1, ms, strides);
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   (void)hipStreamSynchronize(st);
@@ -435,14 +509,16 @@ extern "C" int cloudsc_fields_alloc(int device, int precision, int ngptot, int n
       set_bytes += bytes[n++];
     }
   // two candidate sets and their spacers at most (search_outputs)
-  if (!search_fits(2 * set_bytes + ((size_t)n << 25))) return CLOUDSC_OK;   // no room: no search (method NONE)
+  const size_t budget = search_transient_bytes(set_bytes, n, kPlaceSetsFields);
+  if (!search_fits(budget)) return CLOUDSC_OK;   // no room: no search (method NONE)
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   PlaceCost cost;
   const auto t0 = std::chrono::steady_clock::now();
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
-      hipEventCreate(&e1) != hipSuccess)
-    rc = hip_fail(hipGetLastError(), "fields_alloc stream/events");
+  hipError_t ce = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (ce == hipSuccess) ce = hipEventCreate(&e0);
+  if (ce == hipSuccess) ce = hipEventCreate(&e1);
+  if (ce != hipSuccess) rc = hip_fail(ce, "fields_alloc stream/events");   // the failing call's own error
   auto probe = [&](const cloudsc_fields_t& f) -> float {
     float ms = -1.f;
     cost.launches += 3;
@@ -483,6 +559,7 @@ extern "C" int cloudsc_fields_alloc(int device, int precision, int ngptot, int n
     report->launches = cost.launches;
     report->search_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     report->peak_transient_bytes = cost.peak_bytes;
+    report->transient_budget_bytes = (long long)budget;
     report->method = CLOUDSC_PLACE_METHOD_WRITE_PROBE;
   }
   return CLOUDSC_OK;

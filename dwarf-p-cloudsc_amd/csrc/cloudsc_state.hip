@@ -200,7 +200,7 @@ int field_alloc(cloudsc_gpu_state* s, Arena& ar, void** p, size_t bytes) {
 // field at a time, keeping a candidate only if the kernel time drops by more
 // than 1 % (search_outputs, cloudsc_place.hip: a rejected set is freed at once
 // behind spacers that keep the next set off its pages, rejected single fields
-// are held until the search ends); an allocation failure ends the search with
+// are held until their pass ends); an allocation failure ends the search with
 // the best placement so far.  Outputs are written before the search's launches
 // only by those launches and are reset afterwards: the results do not depend
 // on it (cloudsc_debug_set_placement_search turns it off).
@@ -209,6 +209,8 @@ std::atomic<int> g_place_passes{2};   // cloudsc_debug_set_placement_search
 #define CLOUDSC_PLACE_SETS 8
 #endif
 constexpr int kPlaceSets = CLOUDSC_PLACE_SETS;   // whole fresh output sets tried before the field-by-field passes
+constexpr int kPlaceInputSets = 4;               // input sets (place_inputs): the first in field order, the others
+                                                 // shuffled with spacers
 
 // the KSEG kernel's time on the state's inputs with the output pointers of f:
 // best of 2 timed launches after one untimed, in ms; < 0 on an error
@@ -299,7 +301,6 @@ int place_outputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes,
 // cloudsc_fields_t); member -1 is the pristine plude copy.  A rejected set is
 // freed as soon as it loses; the spacers, held to the end, keep the next
 // candidate off its pages.
-constexpr int kPlaceInputSets = 4;   // the first in field order, the others shuffled with spacers
 int place_inputs(cloudsc_gpu_state* s, const int* members, const size_t* bytes, int n) {
   float best = s->place_final_ms;
   if (!(best > 0.f) || g_place_passes.load() <= 0) return CLOUDSC_OK;
@@ -538,7 +539,12 @@ int cloudsc_state_create(cloudsc_gpu_state_t** out, int device, int precision, i
       if (in.src) in_set += in.bytes;
     // no room for two candidate sets and their spacers next to the state: no
     // search (cloudsc_state_placement_report then says NONE)
-    const bool room = search_fits(2 * std::max(out_set, in_set) + ((size_t)64 << 25));
+    int nin_set = 0;
+    for (const In& in : ins) nin_set += in.src ? 1 : 0;
+    const size_t budget = std::max(search_transient_bytes(out_set, no, kPlaceSets),
+                                   search_transient_bytes(in_set, nin_set, kPlaceInputSets));
+    const bool room = search_fits(budget);
+    if (room) s->pcost.budget_bytes = (long long)budget;
     if (room && (rc = place_outputs(s, members, bytes, no))) return fail(rc);
     // then the inputs (contents copied) and the pristine plude copy
     constexpr int ni = (int)(sizeof(ins) / sizeof(ins[0]));
@@ -607,6 +613,7 @@ int cloudsc_state_placement_report(const cloudsc_gpu_state_t* s, cloudsc_placeme
   r->launches = s->pcost.launches;
   r->search_ms = s->pcost.search_ms;
   r->peak_transient_bytes = s->pcost.peak_bytes;
+  r->transient_budget_bytes = s->pcost.budget_bytes;
   r->method = s->pcost.launches ? CLOUDSC_PLACE_METHOD_KERNEL : CLOUDSC_PLACE_METHOD_NONE;
   return CLOUDSC_OK;
 }

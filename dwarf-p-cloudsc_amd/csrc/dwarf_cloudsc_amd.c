@@ -677,6 +677,17 @@ int main(int argc, char **argv) {
       printf(" ENERGY: shard=%d device=%d n/a (no hwmon power file for this device)\n", d, sh[d].device);
       continue;
     }
+    /* shards sharing a device (--gpus above the device count) read the same
+     * board over overlapping windows: the board's power is not theirs alone
+     * (ADVICE r05), so no per-column figure is claimed */
+    int sharing = 0;
+    for (int e = 0; e < nused; e++) sharing += sh[e].device == sh[d].device;
+    if (sharing > 1) {
+      printf(" ENERGY: shard=%d device=%d board_w=%.1f samples=%d uj_per_column=n/a (the device runs %d shards "
+             "at once; its board power is theirs together)\n", d, sh[d].device, sh[d].board_w,
+             sh[d].power_samples, sharing);
+      continue;
+    }
     printf(" ENERGY: shard=%d device=%d board_w=%.1f samples=%d steps=%d ms_per_step=%.4f uj_per_column=%.3f "
            "source=%s\n", d, sh[d].device, sh[d].board_w, sh[d].power_samples, sh[d].energy_steps,
            sh[d].energy_ms_per_step, sh[d].board_w * sh[d].energy_ms_per_step * 1e3 / sh[d].ngptot,

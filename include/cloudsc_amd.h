@@ -197,6 +197,8 @@ typedef struct cloudsc_placement {
   int method;                             /* CLOUDSC_PLACE_METHOD_*                                  */
   double search_ms;                       /* wall time of the search                                 */
   long long peak_transient_bytes;         /* most device bytes held at once beyond the fields' own   */
+  long long transient_budget_bytes;       /* the bound the free-memory check was made for (round 6):  */
+                                          /* peak_transient_bytes never exceeds it; 0 = no search    */
 } cloudsc_placement_t;
 #define CLOUDSC_PLACE_METHOD_NONE        0   /* no search                                             */
 #define CLOUDSC_PLACE_METHOD_KERNEL      1   /* the KSEG kernel on the state's own inputs (state API)  */
@@ -274,10 +276,12 @@ int cloudsc_debug_fp32_libm(int device, int which, const float *x, const float *
 const char *cloudsc_strerror(int code);
 const char *cloudsc_last_hip_error(void);
 
-/* Measurement: the achievable HBM bandwidth of this device, a STREAM copy of
- * `bytes` (>= 1 MiB) into a second buffer (2 x bytes moved per launch), best
- * of `reps` launches after one warm-up, in GB/s (10^9 B/s).  bench.py reports
- * it as roofline.achievable_peak beside the 8 TB/s spec. */
+/* Measurement: the achievable HBM bandwidth of this device, a STREAM copy
+ * between two buffers of bytes / 2 (>= 1 MiB each; 2 x bytes / 2 moved per
+ * launch) in 16-byte-per-lane tiles, over three such buffer pairs allocated
+ * together (their placement moves the rate by ~5 %), `reps` launches of each
+ * tile shape per pair after one warm-up; the best launch, in GB/s (10^9 B/s).
+ * bench.py reports it as roofline.achievable_peak beside the 8 TB/s spec. */
 int cloudsc_hbm_copy_gbps(int device, long long bytes, int reps, double *gbps);
 
 /* Measurement: the host<->device copy ceiling of this device, the bound of the
@@ -439,6 +443,16 @@ int cloudsc_debug_set_placement_search(int passes);
  * of a field set without its contents (tools/place_corr.py). */
 int cloudsc_debug_memory_probe(int device, int precision, int ngptot, int nproma, int klev,
                                const cloudsc_fields_t *f, int mode, int reps, float *ms);
+
+/* Diagnostic (round 6 layout study, tools/layout_corr.py): the same probe over
+ * fields in another HBM layout.  strides[6] = the element strides between
+ * blocks, between rows (levels) and between species planes of the inputs, then
+ * of the outputs; 0 keeps the reference block layout's.  Each field pointer
+ * addresses row 0 of block 0 (species 0) of its field; every element the
+ * strides address must lie inside that field's allocation. */
+int cloudsc_debug_memory_probe_layout(int device, int precision, int ngptot, int nproma, int klev,
+                                      const cloudsc_fields_t *f, int mode, int reps, const long long *strides,
+                                      float *ms);
 
 /* Diagnostic, diagnostic build only (-DCLOUDSC_DEBUG_CANARY; otherwise
  * CLOUDSC_EINVAL): every device buffer of the states and placement searches

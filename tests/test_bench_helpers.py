@@ -44,3 +44,20 @@ def test_algorithmic_bytes_per_column():
     assert bench.BYTES_PER_COL[8] == (3701 + 3303) * 8 + 4
     assert bench.BYTES_PER_COL[4] == (3701 + 3303) * 4 + 4
     assert bench.IN_BYTES_PER_COL[8] + 3303 * 8 == bench.BYTES_PER_COL[8]
+
+
+def test_launch_histogram_counts_every_launch():
+    import numpy as np
+    ms = [1.650, 1.6551, 1.659, 1.701, 1.862]
+    h = bench.launch_histogram(ms, np)
+    assert h["width_us"] == 10.0 and h["lo_ms"] <= min(ms)
+    assert sum(h["counts"]) == len(ms) and h["counts"][0] >= 1
+    # the slowest launch falls in the last bin
+    assert len(h["counts"]) == int((max(ms) - h["lo_ms"]) * 1e3 // 10.0) + 1
+
+
+def test_host_cores_states_the_cpu_share():
+    h = bench.host_cores()
+    assert h["nproc"] == os.cpu_count() and h["nproc"] >= 1
+    assert h["affinity_cpus"] is None or 1 <= h["affinity_cpus"] <= h["nproc"]
+    assert h["sockets"] is None or h["sockets"] >= 1

@@ -118,7 +118,14 @@ def test_new_entry_points_check_arguments_first(lib):
     lib.cloudsc_debug_kernel_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong]
     assert lib.cloudsc_debug_kernel_copy(None, None, 16) == ca.EINVAL
     assert lib.cloudsc_debug_memory_probe(0, ca.FP64, 1000, 128, 137, None, 0, 1, C.byref(C.c_float())) == ca.EINVAL
-    assert C.sizeof(ca.Placement) == 40
+    lib.cloudsc_debug_memory_probe_layout.argtypes = [C.c_int] * 5 + [C.c_void_p, C.c_int, C.c_int,
+                                                                      C.POINTER(C.c_longlong), C.POINTER(C.c_float)]
+    assert lib.cloudsc_debug_memory_probe_layout(0, ca.FP64, 1000, 128, 137, None, 1, 1, None,
+                                                 C.byref(C.c_float())) == ca.EINVAL
+    neg = (C.c_longlong * 6)(0, 0, 0, -1, 0, 0)
+    assert lib.cloudsc_debug_memory_probe_layout(0, ca.FP64, 1000, 128, 137, C.byref(f), 1, 1, neg,
+                                                 C.byref(C.c_float())) == ca.EINVAL
+    assert C.sizeof(ca.Placement) == 48   # cloudsc_placement_t with transient_budget_bytes (round 6)
 
 
 def test_cli_place_option():
