@@ -276,7 +276,7 @@ def transfer_rate(ca, ds, args, prec, variant, chunk_blocks=128, slots=3):
 def boundary_path(ca, g, ds, args, prec, variant, np, launches=30):
     """The reference CUDA driver's shape on caller-owned buffers: every field
     allocated by cloudsc_fields_alloc (one buffer per field, the outputs placed
-    by the write-pattern search), the inputs copied in (from the state's buffers,
+    by the memory-pattern search), the inputs copied in (from the state's buffers,
     device to device), the KSEG kernel launched through cloudsc_gpu_run on them,
     plude restored before each launch, HIP events on the null stream around each
     launch.  Reports the median kernel time and the search's cost beside the
@@ -327,7 +327,7 @@ def boundary_path(ca, g, ds, args, prec, variant, np, launches=30):
         df.close()
     return {"kernel_ms_median": round(float(np.median(ms)), 4), "kernel_ms_min": round(float(np.min(ms)), 4),
             "launches": len(ms), "placement": rep,
-            "method": "cloudsc_fields_alloc (outputs placed by the write-pattern search) + cloudsc_gpu_run, the "
+            "method": "cloudsc_fields_alloc (outputs placed by the read+write memory-pattern search) + cloudsc_gpu_run, the "
                       "reference CUDA driver's allocate / copy in / launch shape (cloudsc_driver.cu:276-416); "
                       "HIP events on the null stream around each launch (the KSEG prepare kernel included)"}
 

@@ -135,7 +135,7 @@ class Placement(C.Structure):
     def to_dict(self) -> dict:
         return {"probe_first_ms": round(self.probe_first_ms, 4), "probe_final_ms": round(self.probe_final_ms, 4),
                 "tries": self.tries, "moves": self.moves, "launches": self.launches,
-                "method": {0: "none", 1: "kernel", 2: "write-probe"}.get(self.method, self.method),
+                "method": {0: "none", 1: "kernel", 2: "write-probe", 3: "rw-probe"}.get(self.method, self.method),
                 "search_ms": round(self.search_ms, 1), "peak_transient_bytes": self.peak_transient_bytes,
                 "transient_budget_bytes": self.transient_budget_bytes}
 
@@ -777,7 +777,7 @@ class DeviceFields:
     the reference CUDA driver's shape -- allocate (cloudsc_driver.cu:276-328),
     copy the inputs in, launch cloudsc_gpu_run (:391-416), copy the outputs
     back (:425-447) -- with the output buffers placed by the library's
-    write-pattern search unless place=False."""
+    memory-pattern search (reads + writes, no physics) unless place=False."""
 
     def __init__(self, ngptot: int, nproma: int, klev: int, precision: int = FP64, device: int = 0,
                  place: bool = True, aerosols: bool = False):

@@ -22,7 +22,10 @@
  *   libcloudsc_c_amd_gpu.so  (-DCLOUDSC_DROPIN_GPU) cloudsc_host_run on HIP
  *                            device 0: the block is copied to the MI355X,
  *                            computed by the k-caching kernel and copied back
- * Both give the reference kernel's bits (fp64).
+ * Both give the reference kernel's bits (fp64).  A third build,
+ * libcloudsc_c_amd_gpu_prof.so (-DCLOUDSC_DROPIN_PROFILE as well), profiles
+ * every call (cloudsc_host_run_profile) and prints where the time went when
+ * the dwarf exits (tools/dropin_cost.py).
  *
  * Semantics of the call (cloudsc_c.c:19-2587): one NPROMA block of klon
  * columns, of which columns kidia..kfdia (1-based) are computed; arrays are
@@ -35,6 +38,10 @@
  * ignores the value, cloudsc_driver.c:195).
  */
 #include <stdio.h>
+#ifdef CLOUDSC_DROPIN_PROFILE
+#include <pthread.h>
+#include <stdlib.h>
+#endif
 
 #include "cloudsc_c.h"      /* the reference declaration (and yomcst_c.h, yoethf_c.h, yoecldp_c.h) */
 #include "cloudsc_amd.h"
@@ -68,6 +75,24 @@ static void params_from_modules(cloudsc_params_t *p, double ptsphy) {
   T(laericesed) T(laericeauto) T(nbeta)
 #undef T
 }
+
+#ifdef CLOUDSC_DROPIN_PROFILE
+/* the sums of every cloudsc_host_run call of the run, on stderr at exit */
+static void print_profile(void) {
+  cloudsc_host_run_profile_t p;
+  if (cloudsc_host_run_profile(-1, &p) != CLOUDSC_OK) return;
+  fprintf(stderr,
+          "CLOUDSC_C_DROPIN_PROFILE calls=%lld total_ms=%.3f alloc_ms=%.3f setup_ms=%.3f pack_ms=%.3f "
+          "enqueue_ms=%.3f h2d_ms=%.3f kernel_ms=%.3f d2h_ms=%.3f wait_ms=%.3f unpack_ms=%.3f max_call_ms=%.3f\n",
+          p.calls, p.total_ms, p.alloc_ms, p.setup_ms, p.pack_ms, p.enqueue_ms, p.h2d_ms, p.kernel_ms, p.d2h_ms,
+          p.wait_ms, p.unpack_ms, p.max_call_ms);
+}
+static pthread_once_t g_prof_once = PTHREAD_ONCE_INIT;
+static void start_profile(void) {
+  cloudsc_host_run_profile(1, NULL);
+  atexit(print_profile);
+}
+#endif
 
 int cloudsc_c(int kidia, int kfdia, int klon, int klev, double ptsphy, double * restrict v_pt, double * restrict v_pq,
               double * restrict v_tendency_cml_t, double * restrict v_tendency_cml_q, double * restrict v_tendency_cml_a,
@@ -112,6 +137,9 @@ int cloudsc_c(int kidia, int kfdia, int klon, int klev, double ptsphy, double * 
       v_pfsqlf + o, v_pfsqif + o, v_pfcqnng + o, v_pfcqlng + o, v_pfsqrf + o, v_pfsqsf + o, v_pfcqrng + o,
       v_pfcqsng + o, v_pfsqltur + o, v_pfsqitur + o, v_pfplsl + o, v_pfplsn + o, v_pfhpsl + o, v_pfhpsn + o};
   const int ncols = kfdia - kidia + 1;
+#ifdef CLOUDSC_DROPIN_PROFILE
+  pthread_once(&g_prof_once, start_profile);
+#endif
 #ifdef CLOUDSC_DROPIN_GPU
   /* one workgroup per block up to 256 columns, else the persistent kernel */
   const int variant = klon <= 256 ? CLOUDSC_VARIANT_KCACHE : CLOUDSC_VARIANT_KSEG;

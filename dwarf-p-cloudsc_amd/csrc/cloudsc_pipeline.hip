@@ -842,6 +842,7 @@ namespace {
 
 struct HostRunCtx {
   hipStream_t st = nullptr;
+  hipEvent_t ev[4] = {};    // profiling: before H2D, after H2D, after the kernel, after D2H
   char* stage = nullptr;    // pinned host
   char* dbuf = nullptr;     // device, same layout
   size_t cap = 0;
@@ -854,6 +855,15 @@ struct HostRunCtx {
 // Device memory is not released at thread exit (the runtime may be gone by
 // then); cloudsc_host_run_release frees the calling thread's contexts.
 thread_local HostRunCtx* t_host_ctx[kMaxDevices] = {};
+
+// cloudsc_host_run_profile: per-call cost sums over all threads
+std::atomic<bool> g_hr_prof{false};
+std::mutex g_hr_prof_mu;
+cloudsc_host_run_profile_t g_hr_sum{};
+using HrClock = std::chrono::steady_clock;
+double ms_since(HrClock::time_point t0, HrClock::time_point t1) {
+  return std::chrono::duration<double, std::milli>(t1 - t0).count();
+}
 
 // copy the active lanes between a caller's field and its packed image: the full
 // blocks before the last one as one run, then `bsize` lanes of each row of the
@@ -869,16 +879,41 @@ void pack_active(char* img, const char* fld, size_t per, size_t full, size_t row
   }
 }
 
+// Fault in the pages of a caller's output field that pack_active(.., false)
+// will write, while the device works: one byte per page of exactly the bytes
+// the unpack overwrites anyway, read and written back unchanged.  A caller's
+// freshly allocated output arrays (the reference driver's) are untouched
+// pages, and faulting them in during the unpack made it 2-5x slower than the
+// copy itself (profiles/r06/host_run_cost.jsonl); here that cost overlaps the
+// device's H2D + kernel + D2H.  Never touches a byte outside the active lanes.
+void prefault_active(const char* fld, size_t per, size_t full, size_t row, size_t lanes) {
+  constexpr size_t kPage = 4096;
+  auto touch = [](const char* b, size_t n) {
+    volatile char* p = (volatile char*)b;
+    for (size_t o = 0; o < n;) {
+      p[o] = p[o];
+      o += kPage - (((uintptr_t)(b + o)) & (kPage - 1));   // the next page's first byte
+    }
+  };
+  if (full) touch(fld, full);
+  for (size_t off = full; off < full + per; off += row) touch(fld + off, lanes);
+}
+
 }  // namespace
 
 extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngptot, int nproma, int klev,
                                 const cloudsc_params_t* params, const cloudsc_fields_t* host) {
+  const bool prof = g_hr_prof.load(std::memory_order_relaxed);
+  const HrClock::time_point t_start = prof ? HrClock::now() : HrClock::time_point{};
+  HrClock::time_point t_packed{}, t_enq{}, t_synced{};
   int rc = validate_run_args(device, precision, variant, ngptot, nproma, klev);
   if (rc) return rc;
   if (!params || !host || !fields_complete(host)) return CLOUDSC_EINVAL;
   if ((rc = check_params(params))) return rc;
   const bool aer = params->laericesed || params->laericeauto;
   if (aer && (!host->pre_ice || !host->picrit_aer || !host->pnice)) return CLOUDSC_EINVAL;
+  const HrClock::time_point t_a0 = prof ? HrClock::now() : HrClock::time_point{};
+  double alloc_ms = 0.0, scratch_ms = 0.0;
   HIPCHK(hipSetDevice(device));
   HostRunCtx*& ctx = t_host_ctx[device];
   if (!ctx) {
@@ -894,6 +929,7 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
     ctx->cur = *params;
     ctx->have_params = true;
   }
+  if (prof) alloc_ms += ms_since(t_a0, HrClock::now());
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
   const int bsize = ngptot - (nblocks - 1) * nproma;   // active lanes of the last block
   const size_t es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
@@ -911,6 +947,7 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
       if (pass == 0) in_end = total;
     }
   if (total > ctx->cap) {
+    const HrClock::time_point t_g0 = prof ? HrClock::now() : HrClock::time_point{};
     if (ctx->stage) (void)hipHostFree(ctx->stage);
     if (ctx->dbuf) (void)hipFree(ctx->dbuf);
     ctx->stage = ctx->dbuf = nullptr;
@@ -924,7 +961,11 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
       return CLOUDSC_ENOMEM;
     }
     ctx->cap = total;
+    if (prof) alloc_ms += ms_since(t_g0, HrClock::now());
   }
+  if (prof && !ctx->ev[0])
+    for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+  HrClock::time_point t_setup = prof ? HrClock::now() : HrClock::time_point{};
   cloudsc_fields_t dev{};
   void** df = (void**)&dev;
   for (int i = 0; i < kNumFields; i++) {
@@ -937,12 +978,18 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
       pack_active(ctx->stage + off[i], (const char*)hf[i], per, (size_t)(nblocks - 1) * per, (size_t)nproma * eb,
                   (size_t)bsize * eb, true);
   }
+  if (prof) {
+    t_packed = HrClock::now();
+    HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+  }
   HIPCHK(hipMemcpyAsync(ctx->dbuf, ctx->stage, in_end, hipMemcpyHostToDevice, ctx->st));
+  if (prof) HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
   const int vk = variant_kind(variant);
   if (vk == CLOUDSC_VARIANT_SCC || vk == CLOUDSC_VARIANT_KSEG) {
     const long long nb = cloudsc_gpu_scratch_bytes(precision, vk, ngptot, nproma, klev);
     if (nb <= 0) return CLOUDSC_EINVAL;
     if ((size_t)nb > ctx->scratch_bytes) {
+      const HrClock::time_point t_s0 = prof ? HrClock::now() : HrClock::time_point{};
       if (ctx->scratch) (void)hipFree(ctx->scratch);
       ctx->scratch = nullptr;
       ctx->scratch_bytes = 0;
@@ -950,6 +997,10 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
       if (e != hipSuccess) { ctx->scratch = nullptr; hip_fail(e, "hipMalloc"); return CLOUDSC_ENOMEM; }
       ctx->scratch_bytes = (size_t)nb;
       HIPCHK(hipMemsetAsync(ctx->scratch, 0, 256, ctx->st));   // control words (recycled memory)
+      if (prof) {
+        scratch_ms = ms_since(t_s0, HrClock::now());
+        alloc_ms += scratch_ms;
+      }
     }
   }
   rc = gpu_run_impl(device, ctx->st, precision, variant, ngptot, nproma, klev, &dev, ctx->scratch, nullptr,
@@ -958,11 +1009,24 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
     (void)hipStreamSynchronize(ctx->st);
     return rc;
   }
+  if (prof) HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
   // plude (INOUT) sits in the input region: bring back from it to the end
   const int iplude = (int)(offsetof(cloudsc_fields_t, plude) / sizeof(void*));
   HIPCHK(hipMemcpyAsync(ctx->stage + off[iplude], ctx->dbuf + off[iplude], total - off[iplude],
                         hipMemcpyDeviceToHost, ctx->st));
+  if (prof) {
+    HIPCHK(hipEventRecord(ctx->ev[3], ctx->st));
+    t_enq = HrClock::now();
+  }
+  // while the device works: fault in the caller's output pages the unpack will write
+  for (int i = 0; i < kNumFields; i++) {
+    const FieldDesc& d = kFieldTable[i];
+    if (!hf[i] || !(d.dir == FD_OUT || d.dir == FD_INOUT)) continue;
+    const size_t per = per_block_elems(d.kind, nproma, klev) * es;
+    prefault_active((const char*)hf[i], per, (size_t)(nblocks - 1) * per, (size_t)nproma * es, (size_t)bsize * es);
+  }
   HIPCHK(hipStreamSynchronize(ctx->st));
+  if (prof) t_synced = HrClock::now();
   if (vk == CLOUDSC_VARIANT_KSEG && (rc = kseg_check(device, ctx->st, ctx->scratch))) return rc;
   for (int i = 0; i < kNumFields; i++) {
     const FieldDesc& d = kFieldTable[i];
@@ -970,6 +1034,37 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
     const size_t per = per_block_elems(d.kind, nproma, klev) * es;
     pack_active(ctx->stage + off[i], (const char*)hf[i], per, (size_t)(nblocks - 1) * per, (size_t)nproma * es,
                 (size_t)bsize * es, false);
+  }
+  if (prof) {
+    const HrClock::time_point t_end = HrClock::now();
+    float dev_ms[3] = {0.f, 0.f, 0.f};
+    for (int q = 0; q < 3; q++) HIPCHK(hipEventElapsedTime(&dev_ms[q], ctx->ev[q], ctx->ev[q + 1]));
+    std::lock_guard<std::mutex> lk(g_hr_prof_mu);
+    g_hr_sum.calls++;
+    g_hr_sum.alloc_ms += alloc_ms;
+    g_hr_sum.setup_ms += ms_since(t_start, t_setup) - (alloc_ms - scratch_ms);
+    g_hr_sum.pack_ms += ms_since(t_setup, t_packed);
+    g_hr_sum.enqueue_ms += ms_since(t_packed, t_enq) - scratch_ms;
+    g_hr_sum.h2d_ms += dev_ms[0];
+    g_hr_sum.kernel_ms += dev_ms[1];
+    g_hr_sum.d2h_ms += dev_ms[2];
+    g_hr_sum.wait_ms += ms_since(t_enq, t_synced);
+    g_hr_sum.unpack_ms += ms_since(t_synced, t_end);
+    g_hr_sum.total_ms += ms_since(t_start, t_end);
+    g_hr_sum.max_call_ms = std::max(g_hr_sum.max_call_ms, ms_since(t_start, t_end));
+  }
+  return CLOUDSC_OK;
+}
+
+extern "C" int cloudsc_host_run_profile(int mode, cloudsc_host_run_profile_t* out) {
+  if (mode < -1 || mode > 1) return CLOUDSC_EINVAL;
+  std::lock_guard<std::mutex> lk(g_hr_prof_mu);
+  if (mode == 1) {
+    g_hr_sum = cloudsc_host_run_profile_t{};
+    g_hr_prof.store(true);
+  } else {
+    if (out) *out = g_hr_sum;
+    if (mode == -1) g_hr_prof.store(false);
   }
   return CLOUDSC_OK;
 }
@@ -980,6 +1075,8 @@ extern "C" int cloudsc_host_run_release(void) {
     if (!ctx) continue;
     (void)hipSetDevice(d);
     if (ctx->st) { (void)hipStreamSynchronize(ctx->st); (void)hipStreamDestroy(ctx->st); }
+    for (auto& e : ctx->ev)
+      if (e) (void)hipEventDestroy(e);
     if (ctx->stage) (void)hipHostFree(ctx->stage);
     if (ctx->dbuf) (void)hipFree(ctx->dbuf);
     if (ctx->scratch) (void)hipFree(ctx->scratch);

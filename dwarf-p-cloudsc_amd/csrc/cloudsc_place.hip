@@ -280,7 +280,7 @@ bool search_fits(size_t transient) {
 
 // ---------------------------------------------------------------------------
 // Output placement search, shared by the state (probe = the KSEG kernel on the
-// state's inputs) and cloudsc_fields_alloc (probe = the write pattern above,
+// state's inputs) and cloudsc_fields_alloc (probe = the memory pattern above,
 // which needs no contents).  Candidates: `sets` whole fresh output sets (the
 // first in field order, the others shuffled with a spacer of 2-32 MiB before
 // each field, so the fields' relative physical placement changes, not just the
@@ -445,7 +445,7 @@ int cloudsc_impl::memory_probe_strided(int device, int precision, int ngptot, in
 // (src/cloudsc_cuda/cloudsc/cloudsc_driver.cu:276-328) and launches on them
 // (:391-416); cloudsc_gpu_run is that launch.  cloudsc_fields_alloc is the
 // allocation: one device buffer per field, and -- unless the caller runs a
-// single step -- the output buffers placed by the write-pattern probe, which
+// single step -- the output buffers placed by the memory-pattern probe, which
 // needs no field contents, so the caller fills the inputs afterwards.
 // ---------------------------------------------------------------------------
 namespace {
@@ -522,7 +522,11 @@ extern "C" int cloudsc_fields_alloc(int device, int precision, int ngptot, int n
   auto probe = [&](const cloudsc_fields_t& f) -> float {
     float ms = -1.f;
     cost.launches += 3;
-    if (memory_probe(device, st, precision, ngptot, nproma, klev, &f, 0, 2, e0, e1, &ms) != CLOUDSC_OK) return -1.f;
+    // the read + write form (mode 1): with the kernel's write-through stores it
+    // ranks placements at Pearson 0.986 / Spearman 0.988 against the kernel, the
+    // write-only form at 0.980 / 0.939 (profiles/r06/place_corr_sc1_fp64.jsonl);
+    // it reads the caller's own (not yet filled) input buffers, where they will stay
+    if (memory_probe(device, st, precision, ngptot, nproma, klev, &f, 1, 2, e0, e1, &ms) != CLOUDSC_OK) return -1.f;
     return ms;
   };
   // the shader clock leaves its idle level over the first ~25 ms of work
@@ -560,7 +564,7 @@ extern "C" int cloudsc_fields_alloc(int device, int precision, int ngptot, int n
     report->search_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     report->peak_transient_bytes = cost.peak_bytes;
     report->transient_budget_bytes = (long long)budget;
-    report->method = CLOUDSC_PLACE_METHOD_WRITE_PROBE;
+    report->method = CLOUDSC_PLACE_METHOD_RW_PROBE;
   }
   return CLOUDSC_OK;
 }

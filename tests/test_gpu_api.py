@@ -460,7 +460,7 @@ def device_outputs(df, ngptot):
                                                (ca.FP32, ca.VARIANT_KSEG)])
 def test_fields_alloc_reference_driver_shape(lib, ds, precision, variant):
     """The reference CUDA driver's shape on caller-owned buffers: allocate every
-    field (cloudsc_fields_alloc, placed by the write-pattern search), copy the
+    field (cloudsc_fields_alloc, placed by the memory-pattern search), copy the
     host block-layout inputs in, cloudsc_gpu_run, copy the outputs out -- bit
     for bit what the state API computes.  The search's record is consistent,
     and cloudsc_fields_free releases every buffer it made."""
@@ -471,7 +471,7 @@ def test_fields_alloc_reference_driver_shape(lib, ds, precision, variant):
     hip = C.CDLL("libamdhip64.so.7")
     try:
         r = df.report.to_dict()
-        assert r["method"] == "write-probe" and r["launches"] >= 30 and r["search_ms"] > 0, r
+        assert r["method"] == "rw-probe" and r["launches"] >= 30 and r["search_ms"] > 0, r
         assert 0 < r["probe_final_ms"] <= r["probe_first_ms"] and 0 <= r["moves"] <= r["tries"], r
         assert r["tries"] >= 21 and r["peak_transient_bytes"] > 0, r
         # the transient footprint stays within what the free-memory check was made for
