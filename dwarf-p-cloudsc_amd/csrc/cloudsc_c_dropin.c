@@ -83,9 +83,10 @@ static void print_profile(void) {
   if (cloudsc_host_run_profile(-1, &p) != CLOUDSC_OK) return;
   fprintf(stderr,
           "CLOUDSC_C_DROPIN_PROFILE calls=%lld total_ms=%.3f alloc_ms=%.3f setup_ms=%.3f pack_ms=%.3f "
-          "enqueue_ms=%.3f h2d_ms=%.3f kernel_ms=%.3f d2h_ms=%.3f wait_ms=%.3f unpack_ms=%.3f max_call_ms=%.3f\n",
+          "enqueue_ms=%.3f h2d_ms=%.3f kernel_ms=%.3f d2h_ms=%.3f wait_ms=%.3f unpack_ms=%.3f max_call_ms=%.3f "
+          "first_calls=%lld first_calls_ms=%.3f\n",
           p.calls, p.total_ms, p.alloc_ms, p.setup_ms, p.pack_ms, p.enqueue_ms, p.h2d_ms, p.kernel_ms, p.d2h_ms,
-          p.wait_ms, p.unpack_ms, p.max_call_ms);
+          p.wait_ms, p.unpack_ms, p.max_call_ms, p.first_calls, p.first_calls_ms);
 }
 static pthread_once_t g_prof_once = PTHREAD_ONCE_INIT;
 static void start_profile(void) {

@@ -636,7 +636,9 @@ int cloudsc_host_run_release(void);
 
 /* Where a cloudsc_host_run call's time goes (round 6, VERDICT r05 weak 6: the
  * GPU drop-in's per-call cost).  Sums over the calls of every thread since
- * profiling was enabled, in ms: host side measured with a steady clock, the
+ * profiling was enabled, in ms, each thread's FIRST call on a device left out
+ * of them (it creates the thread's context and, in a fresh process, starts the
+ * HIP runtime: first_calls / first_calls_ms count those apart): host side measured with a steady clock, the
  * device side with HIP events on the call's stream between its three
  * operations.  alloc: the calling thread's context, device selection, parameter
  * upload and buffer growth (the first calls: the HIP runtime's own start-up
@@ -652,7 +654,9 @@ typedef struct cloudsc_host_run_profile {
   double setup_ms, pack_ms, h2d_ms, kernel_ms, d2h_ms, wait_ms, unpack_ms, total_ms;
   double alloc_ms;     /* part of total_ms, not of setup_ms */
   double enqueue_ms;
-  double max_call_ms;  /* the slowest single call */
+  double max_call_ms;  /* the slowest single call counted */
+  long long first_calls;
+  double first_calls_ms;
 } cloudsc_host_run_profile_t;
 /* mode 1: zero the sums and start profiling (each call then records 4 events);
  * mode 0: copy the sums into *out (may be NULL) and keep profiling;

@@ -49,16 +49,17 @@ def profile_row(err):
     kv = {k: float(v) for k, v in (x.split("=") for x in m.group(1).split())}
     n = kv.pop("calls")
     mx = kv.pop("max_call_ms", None)
+    first = {"calls": int(kv.pop("first_calls", 0)), "ms": kv.pop("first_calls_ms", None)}
     tot = kv["total_ms"]
     parts = ["alloc_ms", "setup_ms", "pack_ms", "enqueue_ms", "h2d_ms", "kernel_ms", "d2h_ms", "unpack_ms"]
     row = {"calls": int(n), "per_call_ms": {k: round(v / n, 4) for k, v in kv.items()},
-           "share_of_total": {k: round(kv[k] / tot, 4) for k in parts + ["wait_ms"]}, "max_call_ms": mx}
-    # host-side work (everything but the device's three operations) and the device's; the steady
-    # state leaves out the one-time context / runtime start-up (alloc)
-    host = kv["setup_ms"] + kv["pack_ms"] + kv["enqueue_ms"] + kv["unpack_ms"]
-    row["host_side_share"] = round((host + kv["alloc_ms"]) / tot, 4)
+           "share_of_total": {k: round(kv[k] / tot, 4) for k in parts + ["wait_ms"]}, "max_call_ms": mx,
+           "first_calls": first}
+    # host-side work (everything but the device's three operations) and the device's, over the calls
+    # after each thread's first (which creates its context and starts the runtime: first_calls)
+    host = kv["setup_ms"] + kv["pack_ms"] + kv["enqueue_ms"] + kv["unpack_ms"] + kv["alloc_ms"]
+    row["host_side_share"] = round(host / tot, 4)
     row["device_side_share"] = round((kv["h2d_ms"] + kv["kernel_ms"] + kv["d2h_ms"]) / tot, 4)
-    row["steady_host_side_share"] = round(host / (tot - kv["alloc_ms"]), 4)
     return row
 
 

@@ -27,7 +27,7 @@ import cloudsc_amd as ca  # noqa: E402
 class Profile(C.Structure):
     _fields_ = [("calls", C.c_longlong)] + [(n, C.c_double) for n in (
         "setup_ms", "pack_ms", "h2d_ms", "kernel_ms", "d2h_ms", "wait_ms", "unpack_ms", "total_ms", "alloc_ms",
-        "enqueue_ms", "max_call_ms")]
+        "enqueue_ms", "max_call_ms")] + [("first_calls", C.c_longlong), ("first_calls_ms", C.c_double)]
 
 
 def main():
@@ -57,6 +57,8 @@ def main():
             ca.check(lib.cloudsc_host_run_profile(-1, C.byref(pr)))
             row = {"ncols": ncols, "nproma": nproma, "call": i + 1}
             row.update({n: round(getattr(pr, n), 4) for n, _ in Profile._fields_[1:] if n != "max_call_ms"})
+            if pr.first_calls:   # the context's first call is counted apart
+                row["total_ms"] = round(pr.first_calls_ms, 4)
             print(json.dumps(row), flush=True)
         worst = ca.validate_host_state(ds, st)
         print(json.dumps({"ncols": ncols, "nproma": nproma, "worst_rel_l1_vs_reference": worst}), flush=True)
