@@ -423,6 +423,14 @@ def main():
     sclk2 = g.kseg_clock() if kind == ca.VARIANT_KSEG else None
     energy = energy_window(g, variant, cp, pw_file, args.energy_seconds, ncols, np) if args.energy_seconds > 0 \
         else None
+    # ranks sharing one device (a rehearsal with more ranks than GPUs) read the same board over overlapping
+    # windows: its power is theirs together, so no per-column energy is claimed
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    sharing = sum(1 for r in range(local_world) if r % ca.device_count() == device)
+    if energy is not None and sharing > 1:
+        energy["energy_uj_per_column"] = None
+        energy["shared_device_note"] = ("%d ranks run on device %d at once: the board's power is theirs together, "
+                                        "no per-column energy" % (sharing, device))
     if energy is not None:
         # the timed region's own board power only from >= 20 samples (4 samples of a sensor
         # that averages over 1-10 ms meant nothing); 100 launches of 1.65 ms give ~17 at 10 ms
