@@ -532,3 +532,114 @@ def test_fields_alloc_flags_and_free(lib, ds):
     finally:
         ca.check(lib.cloudsc_fields_free(0, C.byref(f)))
     assert not f.pt and not f.pfhpsn
+
+
+# ---- round 6: the layout probe's addressing and cloudsc_host_run's profile ----
+def _layout_module():
+    import importlib.util
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools", "layout_corr.py")
+    spec = importlib.util.spec_from_file_location("layout_corr", p)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+@pytest.mark.parametrize("layout", ["B", "I"])
+def test_memory_probe_layout_writes_exactly_its_elements(lib, layout):
+    """cloudsc_debug_memory_probe_layout (the round-6 layout study's
+    instrument, tools/layout_corr.py) over a per-block (B) or per-row (I)
+    interleaved output arena: every output element the layout addresses holds
+    the probe's value (block + level), and every other byte of the arena keeps
+    its sentinel -- the strides keep each field inside its own chunk, with no
+    overlap and no stray store.  200 columns, NPROMA 64 (a partial last block),
+    KLEV 7."""
+    lc = _layout_module()
+    ngptot, nproma, klev = 200, 64, 7
+    nblocks = (ngptot + nproma - 1) // nproma
+    hip = lc.Hip()
+    f, strides, owned = lc.arena_set(hip, layout, nblocks, nproma, klev, 8)
+    h = hip.h
+    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    out_arena = owned[1]
+    rows = klev + 1
+    if layout == "B":
+        nbytes = nblocks * strides[3] * 8
+        base = out_arena
+    else:
+        nbytes = (nblocks * rows + 1) * strides[4] * 8
+        base = out_arena
+    sentinel = np.full(nbytes // 8, -7.5)
+    assert h.hipMemcpy(base, sentinel.ctypes.data, nbytes, 1) == 0
+    lib.cloudsc_debug_memory_probe_layout.argtypes = [C.c_int] * 5 + [C.POINTER(ca.Fields), C.c_int, C.c_int,
+                                                      C.POINTER(C.c_longlong), C.POINTER(C.c_float)]
+    ms = C.c_float()
+    ca.check(lib.cloudsc_debug_memory_probe_layout(0, ca.FP64, ngptot, nproma, klev, C.byref(f), 0, 1,
+                                                   (C.c_longlong * 6)(*strides), C.byref(ms)))
+    got = np.empty(nbytes // 8)
+    assert h.hipMemcpy(got.ctypes.data, base, nbytes, 2) == 0
+    expect = sentinel.copy()
+    bs, rs, ss = strides[3:6]
+    e0 = lambda p: (p - base) // 8   # noqa: E731  element offset of a field pointer in the arena
+    for b in range(nblocks):
+        lanes = min(nproma, ngptot - b * nproma)
+        for k in range(klev):
+            v = float(b + k)
+            for n in lc.OUT_LEVEL:
+                o = e0(getattr(f, n)) + b * bs + k * rs
+                expect[o:o + lanes] = v
+            for m in range(5):
+                o = e0(f.tendency_loc_cld) + b * bs + m * ss + k * rs
+                expect[o:o + lanes] = v
+            for n in lc.OUT_HALF:
+                o = e0(getattr(f, n)) + b * bs + (k + 1) * rs
+                expect[o:o + lanes] = v
+        for n in lc.OUT_HALF:       # half level 0
+            o = e0(getattr(f, n)) + b * bs
+            expect[o:o + lanes] = float(b)
+    assert np.array_equal(got, expect)
+    for p in owned:
+        h.hipFree(C.c_void_p(p))
+
+
+def test_host_run_profile_accounts_for_each_call(lib, ds):
+    """cloudsc_host_run_profile: after enabling it, N calls of cloudsc_host_run
+    on one thread count as the context's first call (apart) or as profiled
+    calls; the parts of the profiled calls add up to their total, and the
+    device's three operations fit in the enqueue + wait span.  Results are the
+    unprofiled ones, bit for bit."""
+    class Prof(C.Structure):
+        _fields_ = [("calls", C.c_longlong)] + [(n, C.c_double) for n in (
+            "setup_ms", "pack_ms", "h2d_ms", "kernel_ms", "d2h_ms", "wait_ms", "unpack_ms", "total_ms", "alloc_ms",
+            "enqueue_ms", "max_call_ms")] + [("first_calls", C.c_longlong), ("first_calls_ms", C.c_double)]
+    lib.cloudsc_host_run_profile.argtypes = [C.c_int, C.POINTER(Prof)]
+    ncols, nproma = 300, 64
+    p = ca.Params.from_dict(ds.params)
+    outs = []
+    for prof in (False, True):
+        st = ca.make_host_state(ds, ncols, nproma, ca.FP64)
+        f = st.fields()
+        if prof:
+            ca.check(lib.cloudsc_host_run_profile(1, None))
+        plude0 = st.arrays["plude"].copy()
+        for _ in range(4):
+            np.copyto(st.arrays["plude"], plude0)
+            ca.check(lib.cloudsc_host_run(0, ca.FP64, ca.VARIANT_KSEG, ncols, nproma, ds.klev, C.byref(p), C.byref(f)))
+        outs.append({k: st.arrays[k].copy() for k in ca.OUTPUT_FIELDS if k in st.arrays})
+        if prof:
+            r = Prof()
+            ca.check(lib.cloudsc_host_run_profile(-1, C.byref(r)))
+    # this thread's context may already exist (earlier tests): then all 4 calls are profiled
+    assert r.calls + r.first_calls == 4 and r.first_calls <= 1
+    parts = r.alloc_ms + r.setup_ms + r.pack_ms + r.enqueue_ms + r.wait_ms + r.unpack_ms
+    assert abs(parts - r.total_ms) <= 0.01 * r.total_ms + 0.2, (parts, r.total_ms)
+    assert 0 < r.kernel_ms and r.h2d_ms + r.kernel_ms + r.d2h_ms <= r.enqueue_ms + r.wait_ms + 0.2
+    assert r.max_call_ms <= r.total_ms
+    assert all(np.array_equal(outs[0][k].view(np.uint8), outs[1][k].view(np.uint8)) for k in outs[0])
+    # profiling is off again: the sums no longer move
+    st = ca.make_host_state(ds, ncols, nproma, ca.FP64)
+    ca.check(lib.cloudsc_host_run(0, ca.FP64, ca.VARIANT_KSEG, ncols, nproma, ds.klev, C.byref(p),
+                                  C.byref(st.fields())))
+    r2 = Prof()
+    ca.check(lib.cloudsc_host_run_profile(0, C.byref(r2)))
+    assert r2.calls == r.calls and r2.total_ms == r.total_ms
