@@ -844,7 +844,7 @@ namespace {
 struct HostRunCtx {
   hipStream_t st = nullptr;
   hipEvent_t ev[4] = {};    // profiling: before H2D, after H2D, after the kernel, after D2H
-  long long calls = 0;      // calls on this context (the first one is profiled apart)
+  long long calls = 0;      // calls on this context (the one that created it is profiled apart)
   char* stage = nullptr;    // pinned host
   char* dbuf = nullptr;     // device, same layout
   size_t cap = 0;
@@ -947,6 +947,7 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
     ctx->have_params = true;
   }
   if (prof) alloc_ms += ms_since(t_a0, HrClock::now());
+  const bool first_call = ctx->calls++ == 0;   // this call created the context (profiled apart)
   const int nblocks = ngptot / nproma + (ngptot % nproma ? 1 : 0);
   const int bsize = ngptot - (nblocks - 1) * nproma;   // active lanes of the last block
   const size_t es = precision == CLOUDSC_FP64 ? sizeof(double) : sizeof(float);
@@ -1057,7 +1058,7 @@ extern "C" int cloudsc_host_run(int device, int precision, int variant, int ngpt
     float dev_ms[3] = {0.f, 0.f, 0.f};
     for (int q = 0; q < 3; q++) HIPCHK(hipEventElapsedTime(&dev_ms[q], ctx->ev[q], ctx->ev[q + 1]));
     std::lock_guard<std::mutex> lk(g_hr_prof_mu);
-    if (ctx->calls++ == 0) {   // the context's creation (and the runtime's start-up): apart
+    if (first_call) {   // the context's creation (and the runtime's start-up): apart
       g_hr_sum.first_calls++;
       g_hr_sum.first_calls_ms += ms_since(t_start, t_end);
       return CLOUDSC_OK;
