@@ -50,6 +50,9 @@ def main():
     p.add_argument("--ngptot", type=int, default=163840)
     p.add_argument("--rounds", type=int, default=60)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--schedule", action="append", default=[],
+                   help="IDX:NSEG:GRID -- cloudsc_debug_set_kseg_schedule(NSEG, GRID) on library IDX (0-based; "
+                        "0 = the library's default); repeatable")
     p.add_argument("libs", nargs="+")
     a = p.parse_args()
     prec = ca.FP64 if a.precision == "fp64" else ca.FP32
@@ -67,6 +70,9 @@ def main():
     params = ca.Params.from_dict(ds.params)
     for lib in libs:
         ca.check(lib.cloudsc_gpu_init(0, C.byref(params)))
+    for spec in a.schedule:
+        idx, nseg, grid = (int(x) for x in spec.split(":"))
+        ca.check(libs[idx].cloudsc_debug_set_kseg_schedule(nseg, grid))
     nbytes = max(lib.cloudsc_gpu_scratch_bytes(prec, variant, a.ngptot, a.nproma, ds.klev) for lib in libs)
     ws, pristine = C.c_void_p(), C.c_void_p()
     plude_bytes = a.ngptot // a.nproma * a.nproma + (a.nproma if a.ngptot % a.nproma else 0)
