@@ -1,5 +1,5 @@
 # Experiment build (round 6): the compute floor -- every KSEG item reads and writes block (b & 31), so the
-# data stays in the memory-side cache; profiles/r06/compute_memory_floors_fp64.txt.
+# data stays in the memory-side cache; profiles/r06/compute_memory_floors.txt.
 #   python tools/exp_variant.py cmponly32 tools/exp_compute_floor_edits.py -DCLOUDSC_ONLY_KSEG=8
 EDITS = [
 ("cloudsc_kcache.h", """  const size_t u1 = (size_t)b * nproma;                            // [nblocks][nproma]
