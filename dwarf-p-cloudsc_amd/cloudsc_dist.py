@@ -14,6 +14,7 @@ which combine_stats mirrors.
 from __future__ import annotations
 
 import os
+import sys
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -57,6 +58,22 @@ def split_blocks(ngptot: int, nproma: int, nparts: int) -> List[Tuple[int, int]]
     return out
 
 
+def _without_stdout(fn):
+    """Run fn() with file descriptor 1 on /dev/null: gloo's C++ side prints its
+    "[Gloo] Rank r is connected to ..." lines to stdout while the group connects,
+    which would land beside rank 0's one-line JSON result."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    try:
+        os.dup2(devnull, 1)
+        return fn()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
+
+
 class Control:
     """Barrier + max-over-ranks on a host (gloo) process group; a no-op for W=1."""
 
@@ -66,7 +83,8 @@ class Control:
         if topo.world > 1:
             import torch.distributed as dist
             if not dist.is_initialized():
-                dist.init_process_group(backend)
+                # connect (and settle) with stdout muted
+                _without_stdout(lambda: (dist.init_process_group(backend), dist.barrier()))
             self.dist = dist
 
     def barrier(self) -> None:

@@ -61,6 +61,20 @@ def test_gloo_world2_control_path():
                         {"rank": 1, "device": 0, "kernel_ms": 2.5, "col_offset": 1000}]
 
 
+def test_gloo_connect_leaves_stdout_to_rank0():
+    """Under torch.distributed.run (the driver's N>1 launch) gloo's connection
+    messages go to stdout from C++; Control mutes them, so rank 0's one line
+    is the whole of stdout."""
+    import subprocess
+    import sys
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_stdout_child.py")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), child],
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines() == ['{"rank0": true}'], r.stdout
+
+
 def test_single_rank_control_is_noop():
     ctl = cd.Control(cd.Topology(0, 1, 0))
     ctl.barrier()
