@@ -157,6 +157,36 @@ def with_aerosols(ds, seed=11):
     s.reference = {}
     return s
 
+# Input edges: states pushed beyond the shipped data's ranges (condensate down
+# to 1e-200 or subnormal, or up 1000x; no water at all; full cloud cover;
+# temperatures 60 K warmer or 80 K colder; tendencies, mass fluxes 100x;
+# pressures 100x lower), for the parity tests at the edges of the input space.
+EDGE_CASES = ("condensate_1e-200", "condensate_subnormal", "condensate_x1000", "no_water", "full_cover",
+              "hot_plus60K", "cold_minus80K", "tendencies_x100", "pressure_x0.01", "mass_flux_x100")
+
+
+def edge_case(ds, name):
+    """Copy of the state for one of EDGE_CASES."""
+    edits = {
+        "condensate_1e-200": {"pclv": lambda a: a * 1e-200},
+        "condensate_subnormal": {"pclv": lambda a: np.where(a > 0, 1e-310, 0.0)},
+        "condensate_x1000": {"pclv": lambda a: a * 1000.0},
+        "no_water": {"pclv": np.zeros_like, "pq": np.zeros_like, "pa": np.zeros_like},
+        "full_cover": {"pa": np.ones_like},
+        "hot_plus60K": {"pt": lambda a: a + 60.0},
+        "cold_minus80K": {"pt": lambda a: a - 80.0},
+        "tendencies_x100": {k: (lambda a: a * 100.0) for k in ("tendency_tmp_t", "tendency_tmp_q", "tendency_tmp_a",
+                                                                "tendency_tmp_cld")},
+        "pressure_x0.01": {"pap": lambda a: a * 0.01, "paph": lambda a: a * 0.01},
+        "mass_flux_x100": {"pmfu": lambda a: a * 100.0, "pmfd": lambda a: a * 100.0},
+    }[name]
+    s = ds.copy()
+    for k, f in edits.items():
+        s.inputs[k] = np.ascontiguousarray(f(s.inputs[k]))
+    s.reference = {}
+    return s
+
+
 def sliced_levels(ds, lo_lev):
     """The bottom KLEV-lo_lev levels of the state as a standalone column
     (half-level pressures sliced to match)."""
