@@ -635,6 +635,26 @@ def test_bitwise_input_edges(lib, ds, oracle_mod, case):
         assert np.array_equal(a, r), (k, int(np.count_nonzero(a != r)))
 
 
+@pytest.mark.parametrize("case", __import__("make_fixtures").PARAM_CASES)
+def test_bitwise_parameter_edges(lib, ds, oracle_mod, case):
+    """Other time steps and the YRECLDP tuning parameters jittered together
+    (make_fixtures.param_case; the host-folded reciprocals of the known divisors
+    change with them): KSEG and KCACHE bit-identical to the oracle in fp64, and
+    the exact-libm fp32 KSEG kernel to the fp32 restatement."""
+    import make_fixtures as mf
+    s = mf.param_case(ds, case)
+    ref = oracle_outputs(oracle_mod, s, 300, 64)
+    for variant in (ca.VARIANT_KSEG, ca.VARIANT_KCACHE):
+        out = run_gpu(s, 300, 64, variant=variant)
+        assert bitwise_mismatches(out, ref) == {}, variant
+    out = run_gpu(s, 300, 64, precision=ca.FP32, variant=ca.VARIANT_KSEG | ca.FP32_EXACT_LIBM)
+    ref = oracle_outputs(oracle_mod, s, 300, 64, precision=ca.FP32)
+    for _, k in ca.VALIDATED:
+        a = np.ascontiguousarray(out[k], dtype=np.float32).view(np.uint32)
+        r = np.ascontiguousarray(ref[k], dtype=np.float32).view(np.uint32)
+        assert np.array_equal(a, r), (k, int(np.count_nonzero(a != r)))
+
+
 def test_dwarf_tolerance_vs_reference_h5(lib, ds):
     """The dwarf's own printed check (validate_mod.F90:273-290): relL1 of every
     field vs reference.h5 within 10*eps(fp64), no '!!!!' flag."""

@@ -187,6 +187,33 @@ def edge_case(ds, name):
     return s
 
 
+# Parameter edges: other time steps, and the tuning parameters of YRECLDP
+# jittered together (the thermodynamic constants of YOMCST / YOETHF and the
+# integer switches kept), for the parity tests over the parameter space.
+PARAM_CASES = ("ptsphy_60", "ptsphy_900", "ptsphy_1234.567", "ptsphy_7200", "tuning_jitter_1", "tuning_jitter_2")
+THERMO_CONSTANTS = ("rg", "rd", "rcpd", "retv", "rlvtt", "rlstt", "rlmlt", "rtt", "rv", "r2es", "r3les", "r3ies",
+                    "r4les", "r4ies", "r5les", "r5ies", "r5alvcp", "r5alscp", "ralvdcp", "ralsdcp", "ralfdcp",
+                    "rtwat", "rtice", "rticecu", "rtwat_rtice_r", "rtwat_rticecu_r", "rkoop1", "rkoop2", "ptsphy")
+
+
+def param_case(ds, name):
+    """Copy of the state for one of PARAM_CASES: ptsphy_<seconds>, or every
+    float YRECLDP parameter multiplied by its own factor in [0.9, 1.1]
+    (tuning_jitter_<seed>)."""
+    s = ds.copy()
+    s.params = dict(s.params)
+    if name.startswith("ptsphy_"):
+        s.params["ptsphy"] = float(name[len("ptsphy_"):])
+    else:
+        rng = np.random.default_rng(int(name.rsplit("_", 1)[1]))
+        for k in sorted(s.params):
+            v = s.params[k]
+            if k.startswith("r") and k not in THERMO_CONSTANTS and isinstance(v, float):
+                s.params[k] = v * float(rng.uniform(0.9, 1.1))
+    s.reference = {}
+    return s
+
+
 def sliced_levels(ds, lo_lev):
     """The bottom KLEV-lo_lev levels of the state as a standalone column
     (half-level pressures sliced to match)."""
