@@ -67,6 +67,16 @@ def test_cpu_run_other_configurations(ds, oracle_mod, case):
     assert bits_equal(cpu_outputs(s, 300, 32), ca.state_outputs_to_template(ref_st.arrays, 300)) == {}
 
 
+@pytest.mark.parametrize("case", __import__("make_fixtures").EDGE_CASES + __import__("make_fixtures").PARAM_CASES)
+def test_cpu_run_input_and_parameter_edges(ds, oracle_mod, case):
+    """The input-edge states and parameter-edge sets of make_fixtures (the oracle
+    is pinned to the reference kernel on them in tests/test_oracle.py)."""
+    import make_fixtures as mf
+    s = mf.edge_case(ds, case) if case in mf.EDGE_CASES else mf.param_case(ds, case)
+    ref_st, _ = oracle_mod.run_oracle(s, 200, 32)
+    assert bits_equal(cpu_outputs(s, 200, 32), ca.state_outputs_to_template(ref_st.arrays, 200)) == {}
+
+
 def test_cpu_run_threads_and_offset_invariance(ds):
     a = cpu_outputs(ds, 1000, 32, nthreads=1)
     b = cpu_outputs(ds, 1000, 32, nthreads=7)

@@ -618,13 +618,13 @@ def test_bitwise_other_configurations(lib, ds, oracle_mod, case):
 @pytest.mark.parametrize("case", __import__("make_fixtures").EDGE_CASES)
 def test_bitwise_input_edges(lib, ds, oracle_mod, case):
     """States beyond the shipped data's ranges (make_fixtures.edge_case; the oracle
-    is pinned to the reference kernel on them in tests/test_oracle.py): the KSEG
-    and KCACHE kernels bit-identical to the oracle in fp64, and the fp32 kernels
-    with the exact libm bit-identical to the fp32 restatement."""
+    is pinned to the reference kernel on them in tests/test_oracle.py): every
+    variant bit-identical to the oracle in fp64, and the exact-libm fp32 KSEG
+    kernel to the fp32 restatement."""
     import make_fixtures as mf
     s = mf.edge_case(ds, case)
     ref = oracle_outputs(oracle_mod, s, 300, 64)
-    for variant in (ca.VARIANT_KSEG, ca.VARIANT_KCACHE):
+    for variant in (ca.VARIANT_KSEG, ca.VARIANT_KCACHE, ca.VARIANT_SCC, ca.VARIANT_SCC_PRIVATE):
         out = run_gpu(s, 300, 64, variant=variant)
         assert bitwise_mismatches(out, ref) == {}, variant
     out = run_gpu(s, 300, 64, precision=ca.FP32, variant=ca.VARIANT_KSEG | ca.FP32_EXACT_LIBM)
